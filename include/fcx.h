@@ -1,0 +1,114 @@
+/*
+ * fcx.h — C ABI of the MI355X-native LZ77 + Huffman compressor (FCX7 format).
+ *
+ * The reference (YuBinRen/my_compress) has no plugin/FFI surface; its only seam
+ * is the per-block function pair main() calls.  Each entry point below names
+ * the reference interface it replaces (my_compress.cpp, lines counted by '\n'):
+ *
+ *   fcx_compress_block    <- uInt32 my_compress_file_lz77(void*, uInt32, uInt8*)   :2115 (called at :4099)
+ *   fcx_decompress_block  <- uInt32 my_decompress_file_lz77(void*, uInt32, FILE*) :2255 (called at :4182)
+ *   fcx_write_header      <- stCmpFileHead fwrite/rewrite in main()                :101-111, :4079-4086, :4128-4129
+ *   fcx_parse_header      <- header read + "FCX" magic check in main()            :4140-4159
+ *   fcx_compress_shard    <- main()'s per-block compress loop                      :4090-4122
+ *                            (batched: every block of a device-resident shard in one
+ *                             launch sequence, emitting [u32 len][payload]...)
+ *
+ * Conventions: plain pointers and sizes, no exceptions cross the ABI, every
+ * function returns FCX_OK (0) or a negative FCX_ERR_* code unless stated; the
+ * message of the last error on the calling thread is fcx_last_error().  One
+ * host thread per context; functions are reentrant across contexts.
+ * The compress path is GPU-only: without a usable HIP device every compress
+ * entry point fails with FCX_ERR_HIP (there is no CPU fallback).
+ */
+#ifndef FCX_H
+#define FCX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCX_OK 0
+#define FCX_ERR_ARG (-1)       /* NULL pointer, zero/oversize block, bad value */
+#define FCX_ERR_CAPACITY (-2)  /* output buffer too small */
+#define FCX_ERR_HIP (-3)       /* HIP runtime error / no device */
+#define FCX_ERR_FORMAT (-4)    /* malformed compressed stream */
+#define FCX_ERR_INTERNAL (-5)  /* device-side invariant violated */
+#define FCX_ERR_NOMEM (-6)
+
+#define FCX_HEADER_BYTES 10u                 /* "FCX7" + u32 total + u16 blocks (:101-109) */
+#define FCX_DEFAULT_BLOCK_BYTES (1u << 20)  /* BLOCK_BYTES (:113) */
+#define FCX_MAX_BLOCK_BYTES (1u << 20)      /* reference decoder buffer limit (:2373) */
+
+typedef struct fcx_ctx fcx_ctx;
+
+/* ---- per-block drop-in (host buffers) ------------------------------------ */
+
+/* Same contract as my_compress_file_lz77 (:2115): compresses `len` bytes at `in`
+ * (len <= FCX_MAX_BLOCK_BYTES) and writes the block payload to `out`, which the
+ * caller sizes at >= 2*len + 1024 (the reference allots 2 MiB per 1 MiB block,
+ * :4088).  Returns payload bytes, or 0 if a pointer is NULL (:2122-2123) or on
+ * error (see fcx_last_error).  Runs on the current HIP device through a
+ * lazily created per-thread context. */
+uint32_t fcx_compress_block(const void *in, uint32_t len, uint8_t *out);
+
+/* Same contract as my_decompress_file_lz77 (:2255) but into memory: decodes one
+ * block payload of `len` bytes into `out` (capacity `cap`).  Returns decoded
+ * bytes, or a negative FCX_ERR_* code.  Host decoder. */
+int64_t fcx_decompress_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap);
+
+/* ---- container -------------------------------------------------------------- */
+
+/* writes the 10-byte header: "FCX7", u32 total_in mod 2^32, u16 nblocks mod 2^16 */
+int fcx_write_header(uint8_t *out10, uint64_t total_in, uint64_t nblocks);
+/* parses a header; kind receives '7' (LZ77) or '8' (LZ78); FCX_ERR_FORMAT if not "FCX" */
+int fcx_parse_header(const uint8_t *in10, uint32_t *total_in, uint16_t *nblocks, char *kind);
+/* worst-case bytes of fcx_compress_shard's output for n input bytes */
+uint64_t fcx_shard_bound(uint64_t n, uint32_t block_bytes);
+
+/* ---- batched device path ---------------------------------------------------- */
+
+/* Creates a context on HIP device `device` for blocks of `block_bytes`
+ * (1 <= block_bytes <= FCX_MAX_BLOCK_BYTES) and shards up to `max_shard_bytes`;
+ * scratch grows on demand if a later call is larger. */
+int fcx_ctx_create(fcx_ctx **ctx, int device, uint32_t block_bytes, uint64_t max_shard_bytes);
+void fcx_ctx_destroy(fcx_ctx *ctx);
+
+/* Compresses the n device-resident bytes at d_in as consecutive blocks of the
+ * context's block size and writes, contiguously at d_out (device, capacity cap),
+ * [u32 payload_len][payload] for every block in order (no file header).  Work
+ * is enqueued on `stream` (a hipStream_t; NULL = default stream).  If out_len is
+ * non-NULL the call synchronises the stream and stores the byte count there;
+ * the count is always also left in device memory (fcx_ctx_device_out_len). */
+int fcx_compress_shard(fcx_ctx *ctx, const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint64_t cap,
+                       uint64_t *out_len, void *stream);
+/* device address of the u64 output length written by the last fcx_compress_shard */
+const uint64_t *fcx_ctx_device_out_len(fcx_ctx *ctx);
+
+/* Host-to-host convenience for the CLI: compresses host memory in shards of up
+ * to the context's shard size (H2D, device pipeline, D2H) and writes the same
+ * [u32 len][payload]... stream to host `out` (capacity cap). */
+int fcx_compress_host(fcx_ctx *ctx, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap,
+                      uint64_t *out_len);
+
+/* ---- introspection ---------------------------------------------------------- */
+
+/* Enables per-kernel hipEvent timing of subsequent fcx_compress_shard calls. */
+int fcx_ctx_set_profiling(fcx_ctx *ctx, int enable);
+/* After a profiled call: number of stages, and stage i's name and device ms. */
+int fcx_ctx_stage_count(fcx_ctx *ctx);
+int fcx_ctx_stage(fcx_ctx *ctx, int i, const char **name, float *ms);
+/* statistics of the last call (device counters copied back on request):
+ * tokens, matches, lazily evaluated positions, lazy tiles, total tiles */
+int fcx_ctx_stats(fcx_ctx *ctx, uint64_t *tokens, uint64_t *matches, uint64_t *lazy_evals,
+                  uint64_t *lazy_tiles, uint64_t *tiles);
+
+const char *fcx_last_error(void);
+const char *fcx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FCX_H */

@@ -1,0 +1,196 @@
+"""my_compress_amd — MI355X-native LZ77 + Huffman compressor (FCX7 byte stream).
+
+Python mirror of the reference's compress interface over the C ABI in
+include/fcx.h (lib/libfcx.so, hand-written HIP kernels for gfx950):
+
+    my_compress_file_lz77(block) -> payload      # my_compress.cpp:2115
+    my_decompress_file_lz77(payload) -> block    # my_compress.cpp:2255
+    compress(data, block_bytes) -> FCX7 file     # main() compress loop, :4073-4136
+    decompress(blob) -> data                     # main() decompress loop, :4137-4204
+    Context(...).compress_shard(d_in, n, d_out, cap, stream)   # device-resident batch
+
+The compress path runs only on the GPU: a missing extension or device raises
+(FcxError / ImportError); there is no CPU fallback.
+"""
+import ctypes
+import os
+import struct
+
+__all__ = [
+    "FcxError", "lib", "lib_path", "Context", "my_compress_file_lz77", "my_decompress_file_lz77",
+    "compress", "decompress", "shard_bound", "write_header", "BLOCK_BYTES", "HEADER_BYTES",
+]
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+BLOCK_BYTES = 1 << 20   # BLOCK_BYTES, my_compress.cpp:113
+HEADER_BYTES = 10       # stCmpFileHead, my_compress.cpp:101-109
+
+_lib = None
+
+
+class FcxError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return os.path.join(PKG_DIR, "lib", "libfcx.so")
+
+
+def lib():
+    """Load lib/libfcx.so (built by __graft_entry__.build()); raises if missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
+    c_u8p = ctypes.c_void_p
+    L.fcx_compress_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, c_u8p]
+    L.fcx_compress_block.restype = ctypes.c_uint32
+    L.fcx_decompress_block.argtypes = [c_u8p, ctypes.c_uint32, c_u8p, ctypes.c_uint64]
+    L.fcx_decompress_block.restype = ctypes.c_int64
+    L.fcx_write_header.argtypes = [c_u8p, ctypes.c_uint64, ctypes.c_uint64]
+    L.fcx_parse_header.argtypes = [c_u8p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint16),
+                                   ctypes.c_char_p]
+    L.fcx_shard_bound.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+    L.fcx_shard_bound.restype = ctypes.c_uint64
+    L.fcx_ctx_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64]
+    L.fcx_ctx_destroy.argtypes = [ctypes.c_void_p]
+    L.fcx_ctx_destroy.restype = None
+    L.fcx_compress_shard.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+    L.fcx_ctx_device_out_len.argtypes = [ctypes.c_void_p]
+    L.fcx_ctx_device_out_len.restype = ctypes.c_void_p
+    L.fcx_compress_host.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p, ctypes.c_uint64,
+                                    ctypes.POINTER(ctypes.c_uint64)]
+    L.fcx_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.fcx_ctx_stage_count.argtypes = [ctypes.c_void_p]
+    L.fcx_ctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                ctypes.POINTER(ctypes.c_float)]
+    L.fcx_ctx_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
+    L.fcx_last_error.restype = ctypes.c_char_p
+    L.fcx_version.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise FcxError(f"{what} failed ({rc}): {lib().fcx_last_error().decode(errors='replace')}")
+
+
+def shard_bound(n: int, block_bytes: int = BLOCK_BYTES) -> int:
+    return int(lib().fcx_shard_bound(n, block_bytes))
+
+
+def write_header(total_in: int, nblocks: int) -> bytes:
+    buf = ctypes.create_string_buffer(HEADER_BYTES)
+    _check(lib().fcx_write_header(buf, total_in, nblocks), "fcx_write_header")
+    return buf.raw
+
+
+class Context:
+    """fcx_ctx: device, block size, scratch in HBM for shards up to max_shard_bytes."""
+
+    def __init__(self, device: int = 0, block_bytes: int = BLOCK_BYTES, max_shard_bytes: int = BLOCK_BYTES):
+        self._h = ctypes.c_void_p()
+        self.block_bytes = block_bytes
+        _check(lib().fcx_ctx_create(ctypes.byref(self._h), device, block_bytes, max_shard_bytes), "fcx_ctx_create")
+
+    def close(self):
+        if self._h:
+            lib().fcx_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compress_shard(self, d_in: int, n: int, d_out: int, cap: int, stream: int = 0, sync: bool = True):
+        """device pointers in, [u32 len][payload]... at d_out; returns bytes (sync) or None"""
+        out = ctypes.c_uint64(0)
+        _check(lib().fcx_compress_shard(self._h, ctypes.c_void_p(d_in), n, ctypes.c_void_p(d_out), cap,
+                                        ctypes.byref(out) if sync else None, ctypes.c_void_p(stream)),
+               "fcx_compress_shard")
+        return out.value if sync else None
+
+    def device_out_len_ptr(self) -> int:
+        return int(lib().fcx_ctx_device_out_len(self._h))
+
+    def compress_host(self, data: bytes) -> bytes:
+        cap = shard_bound(len(data), self.block_bytes)
+        out = ctypes.create_string_buffer(cap)
+        got = ctypes.c_uint64(0)
+        _check(lib().fcx_compress_host(self._h, data, len(data), out, cap, ctypes.byref(got)), "fcx_compress_host")
+        return out.raw[:got.value]
+
+    def set_profiling(self, on: bool = True):
+        _check(lib().fcx_ctx_set_profiling(self._h, 1 if on else 0), "fcx_ctx_set_profiling")
+
+    def stage_times(self):
+        """[(stage name, device ms)] of the last profiled compress_shard"""
+        res = []
+        for i in range(lib().fcx_ctx_stage_count(self._h)):
+            name = ctypes.c_char_p()
+            ms = ctypes.c_float()
+            _check(lib().fcx_ctx_stage(self._h, i, ctypes.byref(name), ctypes.byref(ms)), "fcx_ctx_stage")
+            res.append((name.value.decode(), ms.value))
+        return res
+
+    def stats(self):
+        vals = [ctypes.c_uint64() for _ in range(5)]
+        _check(lib().fcx_ctx_stats(self._h, *[ctypes.byref(v) for v in vals]), "fcx_ctx_stats")
+        return dict(zip(["tokens", "matches", "lazy_evals", "lazy_tiles", "tiles"], [v.value for v in vals]))
+
+
+def my_compress_file_lz77(block: bytes) -> bytes:
+    """one block (<= 1 MiB) -> payload, same bytes as my_compress_file_lz77 (:2115)"""
+    n = len(block)
+    if n == 0:
+        return b""
+    out = ctypes.create_string_buffer(2 * n + 4096)
+    got = lib().fcx_compress_block(block, n, out)
+    if got == 0:
+        raise FcxError(f"fcx_compress_block failed: {lib().fcx_last_error().decode(errors='replace')}")
+    return out.raw[:got]
+
+
+def my_decompress_file_lz77(payload: bytes, cap: int = BLOCK_BYTES + 8) -> bytes:
+    """payload -> block bytes (reference decoder semantics, :2255)"""
+    out = ctypes.create_string_buffer(cap)
+    got = lib().fcx_decompress_block(payload, len(payload), out, cap)
+    if got < 0:
+        raise FcxError(f"fcx_decompress_block failed ({got})")
+    return out.raw[:got]
+
+
+def compress(data: bytes, block_bytes: int = BLOCK_BYTES, device: int = 0, ctx: "Context" = None) -> bytes:
+    """whole FCX7 file for `data` (header + [u32 len][payload] per block)"""
+    nblocks = (len(data) + block_bytes - 1) // block_bytes
+    if not data:
+        return write_header(0, 0)
+    own = ctx is None
+    if own:
+        ctx = Context(device, block_bytes, min(len(data), 256 << 20))
+    try:
+        body = ctx.compress_host(data)
+    finally:
+        if own:
+            ctx.close()
+    return write_header(len(data), nblocks) + body
+
+
+def decompress(blob: bytes) -> bytes:
+    if len(blob) < HEADER_BYTES or blob[:3] != b"FCX" or blob[3:4] != b"7":
+        raise FcxError("not an FCX7 (LZ77) stream")
+    total, nblocks = struct.unpack_from("<IH", blob, 4)
+    off, out = HEADER_BYTES, []
+    for _ in range(nblocks):
+        (sz,) = struct.unpack_from("<I", blob, off)
+        off += 4
+        out.append(my_decompress_file_lz77(blob[off:off + sz]))
+        off += sz
+    return b"".join(out)

@@ -1,0 +1,154 @@
+// cli.cpp — the my_compress command line (main(), my_compress.cpp:3726-4213),
+// compress path on the GPU through the C ABI.
+//
+//   my_compress -i IN [-o OUT] -c lz77     compress (FCX7, 1 MiB blocks)
+//   my_compress -i IN [-o OUT]             decompress
+//
+// Same flags, default output "./out" (4040-4042) and byte stream as the
+// reference.  Superset: -b/--block BYTES (<= 1 MiB; the reference fixes 1 MiB,
+// BLOCK_BYTES :113) and -d/--device N.  `-c lz78` (the LZ78 codec) is outside
+// this build's scope and is rejected.
+#include <getopt.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fcx.h"
+
+static int usage() {
+    fprintf(stderr,
+            "usage: ./my_compress -i[or --file_in] <input file name> [-o[or --file_out] <output file name>] "
+            "[-c (or --compress) <lz77/lz78>] [-b (or --block) <bytes>] [-d (or --device) <hip device>]\n");
+    return -1;
+}
+
+static int do_compress(FILE *fin, FILE *fout, uint32_t block, int device) {
+    const uint64_t shard = 256ull << 20;  // host staging granule (multiple of any block size <= 1 MiB)
+    const uint64_t shard_blocks = shard / block;
+    const uint64_t shard_bytes = shard_blocks * block;
+    fcx_ctx *ctx = nullptr;
+    if (fcx_ctx_create(&ctx, device, block, shard_bytes)) {
+        fprintf(stderr, "fcx: %s\n", fcx_last_error());
+        return -1;
+    }
+    uint8_t hdr[FCX_HEADER_BYTES];
+    fcx_write_header(hdr, 0, 0);  // placeholder, rewritten at the end (4079-4086, 4128-4129)
+    fwrite(hdr, 1, sizeof(hdr), fout);
+    std::vector<uint8_t> in(shard_bytes), out(fcx_shard_bound(shard_bytes, block));
+    uint64_t total_in = 0, total_out = 0, nblocks = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const size_t got = fread(in.data(), 1, shard_bytes, fin);
+        if (got == 0) break;
+        uint64_t olen = 0;
+        if (fcx_compress_host(ctx, in.data(), got, out.data(), out.size(), &olen)) {
+            fprintf(stderr, "fcx: %s\n", fcx_last_error());
+            fcx_ctx_destroy(ctx);
+            return -1;
+        }
+        fwrite(out.data(), 1, olen, fout);
+        total_in += got;
+        total_out += olen;
+        nblocks += (got + block - 1) / block;
+        if (got < shard_bytes) break;
+    }
+    fcx_write_header(hdr, total_in, nblocks);
+    fseek(fout, 0, SEEK_SET);
+    fwrite(hdr, 1, sizeof(hdr), fout);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    printf("<Final>: LZ77 totalBytes = %llu, compress total bytes=%llu, compress rate: %.2f%%\n",
+           (unsigned long long)total_in, (unsigned long long)total_out,
+           total_in ? 100.0 * (double)total_out / (double)total_in : 0.0);
+    printf("[***TIME***]  All block compress spend %.0f ms!!!\n", ms);
+    if (nblocks > 65535) fprintf(stderr, "warning: %llu blocks exceed the u16 block count of the format\n",
+                                 (unsigned long long)nblocks);
+    fcx_ctx_destroy(ctx);
+    return 0;
+}
+
+static int do_decompress(FILE *fin, FILE *fout) {
+    uint8_t hdr[FCX_HEADER_BYTES];
+    if (fread(hdr, 1, sizeof(hdr), fin) != sizeof(hdr)) {
+        fprintf(stderr, "Read file head infomation error!!!\n");
+        return -1;
+    }
+    uint32_t total = 0;
+    uint16_t nblocks = 0;
+    char kind = 0;
+    if (fcx_parse_header(hdr, &total, &nblocks, &kind)) {
+        fprintf(stderr, "This file is not support to decompress!!!!\n");
+        return -1;
+    }
+    if (kind != '7') {
+        fprintf(stderr, "LZ78 streams are outside this build's scope\n");
+        return -1;
+    }
+    std::vector<uint8_t> payload, plain(FCX_MAX_BLOCK_BYTES + 8);
+    uint64_t got_total = 0;
+    for (uint32_t b = 0; b < nblocks; b++) {
+        uint32_t sz = 0;
+        if (fread(&sz, 4, 1, fin) != 1) return -1;
+        payload.resize(sz);
+        if (fread(payload.data(), 1, sz, fin) != sz) return -1;
+        int64_t n = fcx_decompress_block(payload.data(), sz, plain.data(), plain.size());
+        if (n < 0) {
+            fprintf(stderr, "block %u: %s\n", b + 1, n == FCX_ERR_FORMAT ? "malformed" : "decode error");
+            return -1;
+        }
+        fwrite(plain.data(), 1, (size_t)n, fout);
+        got_total += (uint64_t)n;
+    }
+    // the reference compares sizes only (4198-4201)
+    const bool ok = (uint32_t)got_total == total;
+    printf("All block decompress total bytes = %llu, Compress Before bytes = %u [%s]\n",
+           (unsigned long long)got_total, total, ok ? "SUCCESS" : "FAIL");
+    return ok ? 0 : 1;
+}
+
+int main(int argc, char **argv) {
+    static struct option long_options[] = {{"file_in", required_argument, nullptr, 'i'},
+                                           {"file_out", required_argument, nullptr, 'o'},
+                                           {"compress", required_argument, nullptr, 'c'},
+                                           {"block", required_argument, nullptr, 'b'},
+                                           {"device", required_argument, nullptr, 'd'},
+                                           {nullptr, 0, nullptr, 0}};
+    std::string file_in, file_out = "./out";
+    bool compress = false, lz77 = false;
+    uint32_t block = FCX_DEFAULT_BLOCK_BYTES;
+    int device = 0, opt;
+    if (argc < 3) return usage();
+    while ((opt = getopt_long(argc, argv, "i:o:c:b:d:", long_options, nullptr)) != -1) {
+        switch (opt) {
+        case 'i': file_in = optarg; break;
+        case 'o': file_out = optarg; break;
+        case 'c':
+            compress = true;
+            lz77 = strncmp(optarg, "lz77", 4) == 0;  // any other value means LZ78 (4034-4038)
+            break;
+        case 'b': block = (uint32_t)strtoul(optarg, nullptr, 0); break;
+        case 'd': device = atoi(optarg); break;
+        default: return usage();
+        }
+    }
+    if (file_in.empty()) return usage();
+    if (compress && !lz77) {
+        fprintf(stderr, "-c lz78: the LZ78 codec is outside this build's scope\n");
+        return -1;
+    }
+    if (block == 0 || block > FCX_MAX_BLOCK_BYTES) {
+        fprintf(stderr, "block size must be in [1, %u]\n", FCX_MAX_BLOCK_BYTES);
+        return -1;
+    }
+    FILE *fin = fopen(file_in.c_str(), "rb");
+    if (!fin) { printf("open: %s Fail!!\n", file_in.c_str()); return -1; }
+    FILE *fout = fopen(file_out.c_str(), "wb");
+    if (!fout) { printf("open: %s Fail!!\n", file_out.c_str()); fclose(fin); return -1; }
+    const int r = compress ? do_compress(fin, fout, block, device) : do_decompress(fin, fout);
+    fclose(fin);
+    fclose(fout);
+    return r;
+}

@@ -1,0 +1,376 @@
+// fcx_capi.hip — C ABI of the compress path: context, scratch layout in HBM and
+// the launch sequence.  See include/fcx.h for the contract and the reference
+// interfaces each entry point replaces.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fcx.h"
+#include "fcx_device.h"
+
+namespace fcx {
+void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint32_t *tile_exit,
+                  uint32_t *tile_flags, hipStream_t st);
+void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint32_t *tile_exit,
+                  uint32_t *tile_flags, uint32_t *tile_cnt, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags,
+                  uint8_t *s_chars, uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, int stage, hipEvent_t *ev);
+void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
+                    uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_bits,
+                    uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
+                    hipEvent_t *ev);
+}  // namespace fcx
+
+using namespace fcx;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(FCX_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                       \
+    do {                                                    \
+        hipError_t e_ = (expr);                             \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr);   \
+    } while (0)
+
+inline uint32_t round16(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
+
+const char *kStageNames[] = {"memset",  "match", "stitch",       "tile_count",  "block_scan", "emit",   "hist",
+                             "tree",    "bitcount", "block_layout", "scan_blocks", "zero",       "encode", "headers"};
+constexpr int kNumStages = 14;
+
+Layout make_layout(uint64_t n, uint32_t B) {
+    Layout L;
+    memset(&L, 0, sizeof(L));
+    L.n = n;
+    L.B = B;
+    L.nblocks = (uint32_t)((n + B - 1) / B);
+    L.tpb = (B + kTile - 1) / kTile;
+    L.wpb = (B + 63) / 64;
+    const uint64_t maxmatch = B / 4;
+    L.sstride[0] = round16((B + 7) / 8);                            // literal flags
+    L.sstride[1] = round16(B);                                      // chars
+    L.sstride[2] = round16((kPBits * maxmatch) / 8 + 1 + 8);        // 11-bit distances
+    L.sstride[3] = round16(4 * ((uint64_t)B / 40 + 2) + 16);        // golomb words (<= 0.8 bit/byte)
+    L.cpb_total = 0;
+    for (uint32_t s = 0; s < kStreams; s++) {
+        L.cpb[s] = (L.sstride[s] + kChunk - 1) / kChunk;
+        L.cpb_total += L.cpb[s];
+    }
+    return L;
+}
+}  // namespace
+
+struct fcx_ctx {
+    int device = 0;
+    uint32_t B = 0;
+    uint64_t cap_n = 0;        // shard bytes the scratch is sized for
+    uint32_t cap_blocks = 0;
+    // scratch (device)
+    uint32_t *m = nullptr;
+    uint64_t *chain = nullptr;
+    uint32_t *tile_exit = nullptr, *tile_flags = nullptr, *tile_cnt = nullptr, *tile_off = nullptr;
+    BlockInfo *binfo = nullptr;
+    uint8_t *s[kStreams] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t *hist = nullptr, *ctab = nullptr, *chunk_bits = nullptr;
+    uint8_t *ltab = nullptr, *hhdr = nullptr;
+    uint64_t *blk_off = nullptr;
+    uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits
+    uint64_t *host_words = nullptr;    // pinned mirror
+    // host path staging
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    uint64_t d_in_cap = 0, d_out_cap = 0;
+    hipStream_t own_stream = nullptr;
+    // profiling
+    bool profiling = false;
+    hipEvent_t ev[kNumStages + 1] = {};
+    bool have_times = false;
+    float ms[kNumStages] = {};
+    Layout last{};
+};
+
+namespace {
+void free_scratch(fcx_ctx *c) {
+    void *ptrs[] = {c->m,    c->chain, c->tile_exit, c->tile_flags, c->tile_cnt, c->tile_off, c->binfo,
+                    c->s[0], c->s[1],  c->s[2],      c->s[3],       c->hist,     c->ctab,     c->chunk_bits,
+                    c->ltab, c->hhdr,  c->blk_off};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    c->m = nullptr; c->chain = nullptr; c->tile_exit = c->tile_flags = c->tile_cnt = c->tile_off = nullptr;
+    c->binfo = nullptr;
+    for (auto &p : c->s) p = nullptr;
+    c->hist = c->ctab = c->chunk_bits = nullptr;
+    c->ltab = c->hhdr = nullptr;
+    c->blk_off = nullptr;
+    c->cap_n = 0;
+    c->cap_blocks = 0;
+}
+
+template <typename T>
+int dalloc(T **p, uint64_t bytes, const char *what) {
+    hipError_t e = hipMalloc((void **)p, bytes ? bytes : 16);
+    if (e != hipSuccess) return fail(FCX_ERR_NOMEM, std::string("hipMalloc ") + what + ": " + hipGetErrorString(e));
+    return FCX_OK;
+}
+
+int ensure_scratch(fcx_ctx *c, uint64_t n) {
+    if (n <= c->cap_n) return FCX_OK;
+    free_scratch(c);
+    const Layout L = make_layout(n, c->B);
+    const uint64_t nb = L.nblocks, nt = (uint64_t)L.nblocks * L.tpb;
+    int r;
+    if ((r = dalloc(&c->m, 4ull * nb * c->B, "m"))) return r;
+    if ((r = dalloc(&c->chain, 8ull * nb * L.wpb, "chain"))) return r;
+    if ((r = dalloc(&c->tile_exit, 4 * nt, "tile_exit"))) return r;
+    if ((r = dalloc(&c->tile_flags, 4 * nt, "tile_flags"))) return r;
+    if ((r = dalloc(&c->tile_cnt, 12 * nt, "tile_cnt"))) return r;
+    if ((r = dalloc(&c->tile_off, 12 * nt, "tile_off"))) return r;
+    if ((r = dalloc(&c->binfo, sizeof(BlockInfo) * nb, "binfo"))) return r;
+    for (uint32_t s = 0; s < kStreams; s++)
+        if ((r = dalloc(&c->s[s], (uint64_t)L.sstride[s] * nb + 64, "stream"))) return r;
+    if ((r = dalloc(&c->hist, 4ull * 256 * kStreams * nb, "hist"))) return r;
+    if ((r = dalloc(&c->ctab, 4ull * 256 * kStreams * nb, "ctab"))) return r;
+    if ((r = dalloc(&c->ltab, 256ull * kStreams * nb, "ltab"))) return r;
+    if ((r = dalloc(&c->hhdr, (uint64_t)kHuffHdrStride * kStreams * nb, "hhdr"))) return r;
+    if ((r = dalloc(&c->chunk_bits, 4ull * L.cpb_total * nb, "chunk_bits"))) return r;
+    if ((r = dalloc(&c->blk_off, 8 * nb, "blk_off"))) return r;
+    c->cap_n = (uint64_t)L.nblocks * c->B;
+    c->cap_blocks = L.nblocks;
+    return FCX_OK;
+}
+}  // namespace
+
+extern "C" {
+
+const char *fcx_last_error(void) { return g_err.c_str(); }
+const char *fcx_version(void) { return "fcx-mi355x 0.1 (gfx950)"; }
+
+uint64_t fcx_shard_bound(uint64_t n, uint32_t block_bytes) {
+    if (block_bytes == 0) return 0;
+    const uint64_t nb = (n + block_bytes - 1) / block_bytes;
+    // per block: record/stream headers (<= 4 x 580 + 24) + Huffman words (< 2x input)
+    return 2 * n + nb * 4096 + 64;
+}
+
+int fcx_write_header(uint8_t *out10, uint64_t total_in, uint64_t nblocks) {
+    if (!out10) return fail(FCX_ERR_ARG, "fcx_write_header: NULL");
+    memcpy(out10, "FCX7", 4);
+    const uint32_t t = (uint32_t)total_in;      // cmp_before_bytes wraps (:104)
+    const uint16_t nb = (uint16_t)nblocks;      // block_num is u16 (:105)
+    memcpy(out10 + 4, &t, 4);
+    memcpy(out10 + 8, &nb, 2);
+    return FCX_OK;
+}
+
+int fcx_parse_header(const uint8_t *in10, uint32_t *total_in, uint16_t *nblocks, char *kind) {
+    if (!in10) return fail(FCX_ERR_ARG, "fcx_parse_header: NULL");
+    if (memcmp(in10, "FCX", 3) != 0) return fail(FCX_ERR_FORMAT, "not an FCX stream (:4147)");
+    if (total_in) memcpy(total_in, in10 + 4, 4);
+    if (nblocks) memcpy(nblocks, in10 + 8, 2);
+    if (kind) *kind = (char)in10[3];
+    return FCX_OK;
+}
+
+int fcx_ctx_create(fcx_ctx **out, int device, uint32_t block_bytes, uint64_t max_shard_bytes) {
+    if (!out) return fail(FCX_ERR_ARG, "fcx_ctx_create: NULL ctx");
+    *out = nullptr;
+    if (block_bytes == 0 || block_bytes > FCX_MAX_BLOCK_BYTES)
+        return fail(FCX_ERR_ARG, "block_bytes must be in [1, 1 MiB] (reference decoder limit :2373)");
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) return fail(FCX_ERR_HIP, "no HIP device: the compress path is GPU-only");
+    if (device < 0 || device >= ndev) return fail(FCX_ERR_ARG, "bad device index");
+    HIP_TRY(hipSetDevice(device));
+    fcx_ctx *c = new fcx_ctx();
+    c->device = device;
+    c->B = block_bytes;
+    e = hipHostMalloc((void **)&c->host_words, 64, hipHostMallocDefault);
+    if (e != hipSuccess) { delete c; return hip_fail(e, "hipHostMalloc"); }
+    e = hipMalloc((void **)&c->dev_words, 64);
+    if (e != hipSuccess) { (void)hipHostFree(c->host_words); delete c; return hip_fail(e, "hipMalloc"); }
+    for (int i = 0; i <= kNumStages; i++) (void)hipEventCreate(&c->ev[i]);
+    int r = ensure_scratch(c, max_shard_bytes ? max_shard_bytes : block_bytes);
+    if (r) { fcx_ctx_destroy(c); return r; }
+    *out = c;
+    return FCX_OK;
+}
+
+void fcx_ctx_destroy(fcx_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    free_scratch(c);
+    if (c->dev_words) (void)hipFree(c->dev_words);
+    if (c->host_words) (void)hipHostFree(c->host_words);
+    if (c->d_in) (void)hipFree(c->d_in);
+    if (c->d_out) (void)hipFree(c->d_out);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    for (int i = 0; i <= kNumStages; i++)
+        if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    delete c;
+}
+
+const uint64_t *fcx_ctx_device_out_len(fcx_ctx *c) { return c ? c->dev_words : nullptr; }
+
+int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
+    if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
+    c->profiling = enable != 0;
+    return FCX_OK;
+}
+
+int fcx_ctx_stage_count(fcx_ctx *c) { return c && c->have_times ? kNumStages : 0; }
+
+int fcx_ctx_stage(fcx_ctx *c, int i, const char **name, float *ms) {
+    if (!c || i < 0 || i >= kNumStages) return fail(FCX_ERR_ARG, "bad stage");
+    if (!c->have_times) {
+        HIP_TRY(hipEventSynchronize(c->ev[kNumStages]));
+        for (int k = 0; k < kNumStages; k++) HIP_TRY(hipEventElapsedTime(&c->ms[k], c->ev[k], c->ev[k + 1]));
+        c->have_times = true;
+    }
+    if (name) *name = kStageNames[i];
+    if (ms) *ms = c->ms[i];
+    return FCX_OK;
+}
+
+int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint64_t cap,
+                       uint64_t *out_len, void *stream) {
+    if (!c || !d_out || (n && !d_in)) return fail(FCX_ERR_ARG, "fcx_compress_shard: NULL argument");
+    if (((uintptr_t)d_out & 15) != 0) return fail(FCX_ERR_ARG, "d_out must be 16-byte aligned");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(c->device));
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(c->dev_words, 0, 16, st));
+        if (out_len) *out_len = 0;
+        return FCX_OK;
+    }
+    if (n / c->B >= 65536 * 2048ull) return fail(FCX_ERR_ARG, "shard too large");
+    int r = ensure_scratch(c, n);
+    if (r) return r;
+    const Layout L = make_layout(n, c->B);
+    c->last = L;
+    c->have_times = false;
+    hipEvent_t *ev = c->profiling ? c->ev : nullptr;
+    uint64_t *total = c->dev_words;
+    uint32_t *err = (uint32_t *)(c->dev_words + 1);
+
+    if (ev) HIP_TRY(hipEventRecord(ev[0], st));
+    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 16, st));
+    HIP_TRY(hipMemsetAsync(c->s[0], 0, (uint64_t)L.sstride[0] * L.nblocks, st));
+    HIP_TRY(hipMemsetAsync(c->s[2], 0, (uint64_t)L.sstride[2] * L.nblocks, st));
+    HIP_TRY(hipMemsetAsync(c->s[3], 0, (uint64_t)L.sstride[3] * L.nblocks, st));
+    HIP_TRY(hipMemsetAsync(c->hist, 0, 4ull * 256 * kStreams * L.nblocks, st));
+    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
+    launch_match(d_in, L, c->m, c->chain, c->tile_exit, c->tile_flags, st);
+    if (ev) HIP_TRY(hipEventRecord(ev[2], st));
+    launch_parse(d_in, L, c->m, c->chain, c->tile_exit, c->tile_flags, c->tile_cnt, c->tile_off, c->binfo, c->s[0],
+                 c->s[1], c->s[2], c->s[3], st, 0, ev ? ev + 3 : nullptr);
+    launch_entropy(L, c->binfo, c->s[0], c->s[1], c->s[2], c->s[3], c->hist, c->ctab, c->ltab, c->hhdr,
+                   c->chunk_bits, c->blk_off, total, d_out, cap, err, st, ev ? ev + 7 : nullptr);
+    HIP_TRY(hipGetLastError());
+    if (out_len) {
+        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 16, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        const uint32_t e = (uint32_t)c->host_words[1];
+        if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
+        if (e) return fail(FCX_ERR_INTERNAL, "device invariant violated (error bits " + std::to_string(e) + ")");
+        *out_len = c->host_words[0];
+    }
+    return FCX_OK;
+}
+
+int fcx_ctx_stats(fcx_ctx *c, uint64_t *tokens, uint64_t *matches, uint64_t *lazy_evals, uint64_t *lazy_tiles,
+                  uint64_t *tiles) {
+    if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
+    const uint32_t nb = c->last.nblocks;
+    std::vector<BlockInfo> bi(nb);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (nb) HIP_TRY(hipMemcpy(bi.data(), c->binfo, sizeof(BlockInfo) * nb, hipMemcpyDeviceToHost));
+    uint64_t t = 0, mt = 0, le = 0, lt = 0;
+    for (auto &x : bi) { t += x.ntok; mt += x.nmatch; le += x.lazy_evals; lt += x.lazy_tiles; }
+    if (tokens) *tokens = t;
+    if (matches) *matches = mt;
+    if (lazy_evals) *lazy_evals = le;
+    if (lazy_tiles) *lazy_tiles = lt;
+    if (tiles) {
+        uint64_t tl = 0;
+        for (auto &x : bi) tl += (x.len + kTile - 1) / kTile;
+        *tiles = tl;
+    }
+    return FCX_OK;
+}
+
+int fcx_compress_host(fcx_ctx *c, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    if (!c || (!in && n) || !out) return fail(FCX_ERR_ARG, "fcx_compress_host: NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->own_stream) HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    const uint64_t shard = c->cap_n ? c->cap_n : c->B;
+    const uint64_t need_in = n < shard ? n : shard;
+    const uint64_t need_out = fcx_shard_bound(need_in, c->B);
+    if (c->d_in_cap < need_in) {
+        if (c->d_in) (void)hipFree(c->d_in);
+        c->d_in = nullptr;
+        int r = dalloc(&c->d_in, need_in, "d_in");
+        if (r) return r;
+        c->d_in_cap = need_in;
+    }
+    if (c->d_out_cap < need_out) {
+        if (c->d_out) (void)hipFree(c->d_out);
+        c->d_out = nullptr;
+        int r = dalloc(&c->d_out, need_out, "d_out");
+        if (r) return r;
+        c->d_out_cap = need_out;
+    }
+    uint64_t o = 0;
+    for (uint64_t off = 0; off < n; off += shard) {
+        const uint64_t len = n - off < shard ? n - off : shard;
+        HIP_TRY(hipMemcpyAsync(c->d_in, in + off, len, hipMemcpyHostToDevice, c->own_stream));
+        uint64_t got = 0;
+        int r = fcx_compress_shard(c, c->d_in, len, c->d_out, c->d_out_cap, &got, c->own_stream);
+        if (r) return r;
+        if (o + got > cap) return fail(FCX_ERR_CAPACITY, "fcx_compress_host: output capacity too small");
+        HIP_TRY(hipMemcpyAsync(out + o, c->d_out, got, hipMemcpyDeviceToHost, c->own_stream));
+        HIP_TRY(hipStreamSynchronize(c->own_stream));
+        o += got;
+    }
+    if (out_len) *out_len = o;
+    return FCX_OK;
+}
+
+uint32_t fcx_compress_block(const void *in, uint32_t len, uint8_t *out) {
+    if (!in || !out) return 0;  // :2122-2123
+    if (len == 0) return 0;
+    if (len > FCX_MAX_BLOCK_BYTES) { fail(FCX_ERR_ARG, "block larger than 1 MiB"); return 0; }
+    struct Holder {
+        fcx_ctx *c = nullptr;
+        std::vector<uint8_t> buf;
+        ~Holder() { fcx_ctx_destroy(c); }
+    };
+    thread_local Holder h;
+    if (!h.c) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (fcx_ctx_create(&h.c, dev, FCX_MAX_BLOCK_BYTES, FCX_MAX_BLOCK_BYTES)) return 0;
+    }
+    h.buf.resize(fcx_shard_bound(len, FCX_MAX_BLOCK_BYTES));
+    uint64_t got = 0;
+    if (fcx_compress_host(h.c, (const uint8_t *)in, len, h.buf.data(), h.buf.size(), &got)) return 0;
+    if (got < 4) { fail(FCX_ERR_INTERNAL, "short record"); return 0; }
+    uint32_t plen;
+    memcpy(&plen, h.buf.data(), 4);
+    memcpy(out, h.buf.data() + 4, plen);
+    return plen;
+}
+
+}  // extern "C"

@@ -1,0 +1,442 @@
+// fcx_entropy.hip — Huffman sub-streams and block-record assembly (gfx950).
+//
+// Each block payload carries four Huffman sub-streams (my_huffman_encode_char,
+// my_compress.cpp:987-1104): the literal-flag bitmap (only when > 1 byte,
+// 2095-2108), the chars of every token, the 11-bit packed distances and the
+// golomb words.  The reference tree is NOT canonical:
+//   leaves = symbols with weight > 0, stably sorted by (weight, symbol) (458-498);
+//   each step merges list[0] (left) and list[1] (right) and re-inserts the sum
+//   after every entry of weight <= sum (strict '<' at 588).
+// Because merged weights never decrease, that list is exactly the stable merge
+// of two FIFO queues — sorted leaves and internal nodes in creation order —
+// taking the leaf on a weight tie.  k_tree runs that two-queue form in one wave
+// per (block, stream), then serialises the tree (1013-1066) and the code table:
+// code = root->leaf path, left = 0, root decision in bit 0 (LSB-first, 869-924).
+//
+//   k_hist         256-bin histograms per (block, stream), per-wave LDS bins
+//   k_tree         tree + header bytes + code table + code-word count W
+//   k_bitcount     code bits per 8192-symbol chunk
+//   k_block_layout chunk bit offsets, record layout and size per block
+//   k_scan_blocks  record offsets across the shard (+ capacity check)
+//   k_zero         zero the output bytes the encoder ORs into
+//   k_encode       pack codes of a chunk into LDS words, store them at the
+//                  record's (unaligned) byte offset: interior words plain,
+//                  chunk-edge words atomicOr
+//   k_headers      lengths, counts and tree headers of every record
+#include "fcx_device.h"
+
+namespace fcx {
+
+constexpr uint32_t kErrCodeLen = 1u, kErrBitCount = 2u, kErrCapacity = 4u;
+
+__device__ inline bool stream_active(const BlockInfo &bi, uint32_t s) {
+    if (s == 0) return bi.slen[0] > 1;   // flags are Huffman-coded only when > 1 byte
+    if (s == 3) return bi.gbits > 0;     // no golomb words -> nothing written (989-990)
+    return true;
+}
+
+__device__ inline void chunk_of(const Layout &L, uint32_t r, uint32_t &s, uint32_t &c) {
+    s = 0;
+    while (s < kStreams - 1 && r >= L.cpb[s]) { r -= L.cpb[s]; s++; }
+    c = r;
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hist(Layout L, const BlockInfo *__restrict__ binfo,
+                                              const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
+                                              const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
+                                              uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[4][256];
+    const uint32_t tid = threadIdx.x, wv = tid >> 6;
+    const uint32_t b = blockIdx.x / L.cpb_total;
+    uint32_t s, c;
+    chunk_of(L, blockIdx.x % L.cpb_total, s, c);
+    const BlockInfo &bi = binfo[b];
+    if (!stream_active(bi, s)) return;
+    const uint32_t len = bi.slen[s], c0 = c * kChunk;
+    if (c0 >= len) return;
+    const uint32_t c1 = min(len, c0 + kChunk);
+    const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
+    const uint32_t *w4 = (const uint32_t *)base;
+    for (uint32_t x = tid; x < 1024; x += 256) (&h[0][0])[x] = 0;
+    __syncthreads();
+    for (uint32_t wi = (c0 >> 2) + tid; 4 * wi < c1; wi += 256) {
+        const uint32_t v = w4[wi];
+        const uint32_t nb = min(4u, c1 - 4 * wi);
+        for (uint32_t q = 0; q < nb; q++) atomicAdd(&h[wv][(v >> (8 * q)) & 0xFF], 1u);
+    }
+    __syncthreads();
+    const uint32_t tot = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    if (tot) atomicAdd(&hist[(b * kStreams + s) * 256 + tid], tot);
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_tree(const uint32_t *__restrict__ hist, BlockInfo *__restrict__ binfo,
+                                             uint32_t *__restrict__ ctab, uint8_t *__restrict__ ltab,
+                                             uint8_t *__restrict__ hhdr, uint32_t *__restrict__ err) {
+    __shared__ uint32_t w[256], sw[256], ss[256];
+    __shared__ uint32_t iw[256], il[256], ir[256], par[512];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x / kStreams, s = blockIdx.x % kStreams;
+    BlockInfo &bi = binfo[b];
+    if (!stream_active(bi, s)) {
+        if (lane == 0) { bi.hdrlen[s] = 0; bi.nwords[s] = 0; }
+        return;
+    }
+    const uint32_t hb = (b * kStreams + s) * 256;
+    uint32_t real = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t v = hist[hb + lane + 64 * q];
+        w[lane + 64 * q] = v;
+        real += (uint32_t)__popcll(__ballot(v != 0));
+    }
+    __syncthreads();
+    // stable sort of the leaves by (weight, symbol): rank = number of smaller keys
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t sym = lane + 64 * q, wt = w[sym];
+        if (wt) {
+            const uint64_t key = ((uint64_t)wt << 8) | sym;
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < 256; j++) {
+                const uint32_t wj = w[j];
+                rank += (wj != 0 && (((uint64_t)wj << 8) | j) < key) ? 1u : 0u;
+            }
+            sw[rank] = wt;
+            ss[rank] = sym;
+        }
+    }
+    __syncthreads();
+    const uint32_t nint = real >= 2 ? real - 1 : 0;
+    if (lane == 0 && nint) {
+        // two-queue merge == the reference's sorted-list re-insertion (570-611)
+        uint32_t lq = 0, iq = 0;
+        for (uint32_t kk = 0; kk < nint; kk++) {
+            uint32_t id[2], wt[2];
+            for (int h = 0; h < 2; h++) {
+                if (lq < real && (iq >= kk || sw[lq] <= iw[iq])) { id[h] = ss[lq]; wt[h] = sw[lq]; lq++; }
+                else { id[h] = 256 + iq; wt[h] = iw[iq]; iq++; }
+            }
+            iw[kk] = wt[0] + wt[1];
+            il[kk] = id[0];
+            ir[kk] = id[1];
+            par[id[0]] = 256 + kk;
+            par[id[1]] = 256 + kk;
+        }
+    }
+    __syncthreads();
+    const uint32_t root = 256 + nint - 1;
+    uint64_t bits = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t sym = lane + 64 * q;
+        uint32_t code = 0, len = 0;
+        if (nint && w[sym]) {
+            uint32_t cur = sym;
+            while (cur != root && len <= 32) {
+                const uint32_t p = par[cur];
+                code = (code << 1) | (ir[p - 256] == cur ? 1u : 0u);
+                len++;
+                cur = p;
+            }
+            if (len > 32) atomicOr(err, kErrCodeLen);
+        }
+        ctab[hb + sym] = code;
+        ltab[hb + sym] = (uint8_t)len;
+        bits += (uint64_t)w[sym] * len;
+    }
+    bits = wave_sum_u64(bits);
+    // header: [u8 ts][ceil(2ts/8) B internal-child bitmap][ts x (u8 l, u8 r)]
+    const uint32_t ts = nint, nbm = (2 * ts + 7) / 8;
+    uint8_t *hdr = hhdr + (uint64_t)(b * kStreams + s) * kHuffHdrStride;
+    if (lane == 0) hdr[0] = (uint8_t)ts;
+    if (lane < nbm) {
+        uint32_t byte = 0;
+        for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t node = (8 * lane + q) >> 1;
+            if (node < ts) {
+                const uint32_t ch = (q & 1) ? ir[node] : il[node];
+                if (ch >= 256) byte |= 1u << q;
+            }
+        }
+        hdr[1 + lane] = (uint8_t)byte;
+    }
+    for (uint32_t kk = lane; kk < ts; kk += 64) {
+        const uint32_t l = il[kk], r = ir[kk];
+        hdr[1 + nbm + 2 * kk] = (uint8_t)(l >= 256 ? (256 - real) + (l - 256) : l);
+        hdr[1 + nbm + 2 * kk + 1] = (uint8_t)(r >= 256 ? (256 - real) + (r - 256) : r);
+    }
+    if (lane == 0) {
+        bi.hdrlen[s] = 1 + nbm + 2 * ts;
+        bi.nwords[s] = (uint32_t)((bits + 31) / 32);
+    }
+}
+
+// ---------------------------------------------------------------------------
+__device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32_t i1, uint32_t *out32 /*8 words*/) {
+    // loads the (up to) 32 symbols [i0, i1) as 8 words, masked past i1
+    const uint32_t n = i1 > i0 ? i1 - i0 : 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) out32[q] = (4 * q < n) ? w4[(i0 >> 2) + q] : 0u;
+    return n;
+}
+
+__global__ __launch_bounds__(256) void k_bitcount(Layout L, const BlockInfo *__restrict__ binfo,
+                                                  const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
+                                                  const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
+                                                  const uint8_t *__restrict__ ltab, uint32_t *__restrict__ chunk_bits) {
+    __shared__ uint32_t lt[256];
+    __shared__ uint32_t red[4];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x / L.cpb_total, r = blockIdx.x % L.cpb_total;
+    uint32_t s, c;
+    chunk_of(L, r, s, c);
+    const BlockInfo &bi = binfo[b];
+    const uint32_t len = bi.slen[s], c0 = c * kChunk;
+    if (!stream_active(bi, s) || c0 >= len) {
+        if (tid == 0) chunk_bits[blockIdx.x] = 0;
+        return;
+    }
+    const uint32_t c1 = min(len, c0 + kChunk);
+    lt[tid] = ltab[(b * kStreams + s) * 256 + tid];
+    __syncthreads();
+    const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
+    const uint32_t i0 = c0 + 32 * tid, i1 = min(c1, i0 + 32);
+    uint32_t sym[8];
+    const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
+    uint32_t nb = 0;
+    for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
+    nb = wave_sum_u32(nb);
+    if ((tid & 63) == 0) red[tid >> 6] = nb;
+    __syncthreads();
+    if (tid == 0) chunk_bits[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// record layout of one block: offsets relative to the record start
+struct RecLayout {
+    uint32_t hdr_rel[kStreams];    // tree header (or raw flag bytes for s=0 when not Huffman-coded)
+    uint32_t words_rel[kStreams];  // first code word
+    uint32_t n_rel, pcnt_rel, g_rel, rec_bytes;
+};
+
+__device__ inline RecLayout record_layout(const BlockInfo &bi) {
+    RecLayout R;
+    uint32_t o = 4;          // u32 payload length (written by main(), 4112)
+    R.n_rel = o; o += 4;     // u32 N (2137-2139)
+    for (uint32_t s = 0; s < kStreams; s++) {
+        if (s == 2) { R.pcnt_rel = o; o += 4; }  // u32 pCnt (2187-2189)
+        if (s == 3) { R.g_rel = o; o += 4; }     // u32 golombLen (2226-2228)
+        R.hdr_rel[s] = o;
+        if (s == 0 && bi.slen[0] <= 1) {          // raw flag byte(s) (2103-2107)
+            R.words_rel[0] = o;
+            o += bi.slen[0];
+        } else if (s == 3 && bi.gbits == 0) {
+            R.words_rel[3] = o;
+        } else {
+            o += bi.hdrlen[s];
+            o += 4;          // u32 W
+            R.words_rel[s] = o;
+            o += 4 * bi.nwords[s];
+        }
+    }
+    R.rec_bytes = o;
+    return R;
+}
+
+__global__ __launch_bounds__(64) void k_block_layout(Layout L, BlockInfo *__restrict__ binfo,
+                                                     uint32_t *__restrict__ chunk_bits, uint32_t *__restrict__ err) {
+    const uint32_t lane = threadIdx.x, b = blockIdx.x;
+    BlockInfo &bi = binfo[b];
+    if (lane < kStreams) {
+        const uint32_t s = lane;
+        uint32_t r0 = 0;
+        for (uint32_t q = 0; q < s; q++) r0 += L.cpb[q];
+        uint32_t run = 0;
+        for (uint32_t c = 0; c < L.cpb[s]; c++) {
+            uint32_t &cb = chunk_bits[(uint64_t)b * L.cpb_total + r0 + c];
+            const uint32_t v = cb;
+            cb = run;                       // -> exclusive bit offset of the chunk
+            run += v;
+        }
+        if (stream_active(bi, s) && (run + 31) / 32 != bi.nwords[s]) atomicOr(err, kErrBitCount);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        const RecLayout R = record_layout(bi);
+        for (uint32_t s = 0; s < kStreams; s++) bi.words_rel[s] = R.words_rel[s];
+        bi.rec_bytes = R.rec_bytes;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t nblocks, const BlockInfo *__restrict__ binfo,
+                                                      uint64_t *__restrict__ blk_off, uint64_t *__restrict__ total,
+                                                      uint64_t cap, uint32_t *__restrict__ err) {
+    __shared__ uint64_t wsum[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint64_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += 1024) {
+        const uint32_t b = b0 + tid;
+        const uint64_t v = b < nblocks ? binfo[b].rec_bytes : 0;
+        uint64_t inc = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t lo = __shfl_up((uint32_t)inc, o, 64), hi = __shfl_up((uint32_t)(inc >> 32), o, 64);
+            if (lane >= (uint32_t)o) inc += ((uint64_t)hi << 32) | lo;
+        }
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        uint64_t pre = carry, all = carry;
+        for (uint32_t q = 0; q < 16; q++) {
+            if (q < wv) pre += wsum[q];
+            all += wsum[q];
+        }
+        if (b < nblocks) blk_off[b] = pre + inc - v;
+        carry = all;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        *total = carry;
+        if (carry > cap) atomicOr(err, kErrCapacity);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_zero(uint8_t *__restrict__ out, const uint64_t *__restrict__ total,
+                                              const uint32_t *__restrict__ err) {
+    if (*err & kErrCapacity) return;
+    const uint64_t n = *total;
+    const uint64_t n16 = n >> 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint4 *o16 = (uint4 *)out;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) o16[i] = make_uint4(0, 0, 0, 0);
+    if (blockIdx.x == 0 && threadIdx.x < (n & 15)) out[(n16 << 4) + threadIdx.x] = 0;
+}
+
+constexpr uint32_t kEncWords = kChunk + 2;  // codes <= 32 bits
+
+__global__ __launch_bounds__(256) void k_encode(Layout L, const BlockInfo *__restrict__ binfo,
+                                                const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
+                                                const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
+                                                const uint32_t *__restrict__ ctab, const uint8_t *__restrict__ ltab,
+                                                const uint32_t *__restrict__ chunk_off,
+                                                const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
+                                                const uint32_t *__restrict__ err) {
+    __shared__ uint32_t ct[256], lt[256];
+    __shared__ uint32_t ws[kEncWords];
+    __shared__ uint32_t red[4];
+    if (*err) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t b = blockIdx.x / L.cpb_total, r = blockIdx.x % L.cpb_total;
+    uint32_t s, c;
+    chunk_of(L, r, s, c);
+    const BlockInfo &bi = binfo[b];
+    const uint32_t len = bi.slen[s], c0 = c * kChunk;
+    if (!stream_active(bi, s) || c0 >= len) return;
+    const uint32_t c1 = min(len, c0 + kChunk);
+    const uint32_t hb = (b * kStreams + s) * 256;
+    ct[tid] = ctab[hb + tid];
+    lt[tid] = ltab[hb + tid];
+    __syncthreads();
+    const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
+    const uint32_t i0 = c0 + 32 * tid, i1 = min(c1, i0 + 32);
+    uint32_t sym[8];
+    const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
+    uint32_t nb = 0;
+    for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
+    // block exclusive scan of nb
+    const uint32_t inc = wave_incl_scan(nb);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0, ctot = 0;
+    for (uint32_t q = 0; q < 4; q++) {
+        if (q < wv) pre += red[q];
+        ctot += red[q];
+    }
+    const uint32_t tb = pre + inc - nb;
+    const uint64_t obyte = blk_off[b] + bi.words_rel[s];
+    const uint64_t g0 = 8 * obyte + chunk_off[(uint64_t)b * L.cpb_total + r];
+    const uint64_t gw = g0 >> 5;
+    const uint32_t sh0 = (uint32_t)(g0 & 31);
+    const uint32_t nw = (sh0 + ctot + 31) >> 5;
+    for (uint32_t x = tid; x < nw; x += 256) ws[x] = 0;
+    __syncthreads();
+    uint32_t pos = sh0 + tb, wi = pos >> 5, ap = pos & 31;
+    uint64_t acc = 0;
+    for (uint32_t q = 0; q < n; q++) {
+        const uint32_t sy = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
+        acc |= (uint64_t)ct[sy] << ap;
+        ap += lt[sy];
+        while (ap >= 32) {
+            atomicOr(&ws[wi], (uint32_t)acc);
+            acc >>= 32;
+            ap -= 32;
+            wi++;
+        }
+    }
+    if (ap) atomicOr(&ws[wi], (uint32_t)acc);
+    __syncthreads();
+    uint32_t *o32 = (uint32_t *)out + gw;
+    for (uint32_t x = tid; x < nw; x += 256) {
+        const uint32_t v = ws[x];
+        if (x == 0 || x == nw - 1) { if (v) atomicOr(&o32[x], v); }
+        else o32[x] = v;
+    }
+}
+
+__device__ inline void put_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t lane) {
+    for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+}
+__device__ inline void put_u32(uint8_t *dst, uint32_t v, uint32_t lane) {
+    if (lane < 4) dst[lane] = (uint8_t)(v >> (8 * lane));
+}
+
+__global__ __launch_bounds__(64) void k_headers(const BlockInfo *__restrict__ binfo, const uint8_t *__restrict__ s0,
+                                                uint32_t s0_stride, const uint8_t *__restrict__ hhdr,
+                                                const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
+                                                const uint32_t *__restrict__ err) {
+    if (*err) return;
+    const uint32_t lane = threadIdx.x, b = blockIdx.x;
+    const BlockInfo &bi = binfo[b];
+    const RecLayout R = record_layout(bi);
+    uint8_t *rec = out + blk_off[b];
+    put_u32(rec, R.rec_bytes - 4, lane);
+    put_u32(rec + R.n_rel, bi.ntok, lane);
+    put_u32(rec + R.pcnt_rel, bi.nmatch, lane);
+    put_u32(rec + R.g_rel, (bi.gbits + 31) / 32, lane);
+    for (uint32_t s = 0; s < kStreams; s++) {
+        if (s == 0 && bi.slen[0] <= 1) {
+            put_bytes(rec + R.hdr_rel[0], s0 + (uint64_t)b * s0_stride, bi.slen[0], lane);
+            continue;
+        }
+        if (s == 3 && bi.gbits == 0) continue;
+        const uint8_t *h = hhdr + (uint64_t)(b * kStreams + s) * kHuffHdrStride;
+        put_bytes(rec + R.hdr_rel[s], h, bi.hdrlen[s], lane);
+        put_u32(rec + R.hdr_rel[s] + bi.hdrlen[s], bi.nwords[s], lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
+void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
+                    uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_bits,
+                    uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
+                    hipEvent_t *ev) {
+    const uint32_t nchunks = L.nblocks * L.cpb_total;
+    hipLaunchKernelGGL(k_hist, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, hist);
+    if (ev) (void)hipEventRecord(ev[0], st);
+    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(64), 0, st, hist, binfo, ctab, ltab, hhdr, err);
+    if (ev) (void)hipEventRecord(ev[1], st);
+    hipLaunchKernelGGL(k_bitcount, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, ltab, chunk_bits);
+    if (ev) (void)hipEventRecord(ev[2], st);
+    hipLaunchKernelGGL(k_block_layout, dim3(L.nblocks), dim3(64), 0, st, L, binfo, chunk_bits, err);
+    if (ev) (void)hipEventRecord(ev[3], st);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, L.nblocks, binfo, blk_off, total, cap, err);
+    if (ev) (void)hipEventRecord(ev[4], st);
+    hipLaunchKernelGGL(k_zero, dim3(2048), dim3(256), 0, st, out, total, err);
+    if (ev) (void)hipEventRecord(ev[5], st);
+    hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, chunk_bits,
+                       blk_off, out, err);
+    if (ev) (void)hipEventRecord(ev[6], st);
+    hipLaunchKernelGGL(k_headers, dim3(L.nblocks), dim3(64), 0, st, binfo, s0, L.sstride[0], hhdr, blk_off, out, err);
+    if (ev) (void)hipEventRecord(ev[7], st);
+}
+
+}  // namespace fcx

@@ -1,0 +1,375 @@
+// fcx_parse.hip — greedy-parse resolution across tiles and token emission (gfx950).
+//
+// The reference parse (my_LZ77_compress, my_compress.cpp:1675-1714) is one serial
+// chain: cursor += l + 1.  k_match resolved it inside each tile under the
+// assumption that a token starts at the tile's first position.  Here:
+//
+//   k_stitch      one wave per block walks the tiles in order with the true entry
+//                 point.  Fast path: the entry lies on the tile's speculative chain,
+//                 so the rest of the tile is already right (clear the bits before
+//                 it, jump to the tile exit).  Slow path: walk the true chain through
+//                 the tile's m[] (staged in LDS) until it meets the speculative chain;
+//                 positions k_match left unknown (dense windows) are evaluated here
+//                 by the whole wave: 64 candidates per step, oldest first, pruned by
+//                 the byte at the current best length, early exit at the cap.
+//   k_tile_count  tokens / matches / golomb bits per tile.
+//   k_block_scan  per-block exclusive scans of those counts + stream lengths.
+//   k_emit        writes the four streams of the block payload (make_bitMap_table
+//                 2073-2113, the split at 2150-2161, combine_bits 1292-1313,
+//                 golomb_rice_encode 258-304), staging bit words in LDS.
+#include "fcx_device.h"
+
+namespace fcx {
+
+// ---------------------------------------------------------------------------
+// wave-parallel exact match at position t (block-relative), window data in LDS
+// image `dw` whose byte 0 is block position dbase.
+__device__ uint32_t lazy_match(const uint32_t *dw, uint32_t dbase, uint32_t blen, uint32_t t) {
+    if (t == 0 || blen - t < 4) return 0;
+    const uint32_t lane = lane_id();
+    const uint32_t cap = min(kMaxL, blen - t) - 1;
+    const uint32_t x = t - dbase;
+    const uint32_t xlo = (t > kWin ? t - kWin : 0) - dbase;
+    const uint32_t key = lds_key3(dw, x);
+    uint32_t best = kMinL - 1, bestx = x;
+    for (uint32_t cb = xlo; cb < x; cb += 64) {
+        const uint32_t xe = cb + lane;
+        uint32_t Lc = 0;
+        if (xe < x && lds_key3(dw, xe) == key &&
+            (best < kMinL || lds_ld1(dw, xe + best) == lds_ld1(dw, x + best)))
+            Lc = lds_match_len(dw, xe, x, kMinL, cap);
+        const uint32_t mx = wave_max_u32(Lc);
+        if (mx > best) {
+            const uint64_t msk = __ballot(Lc == mx);
+            bestx = cb + (uint32_t)(__ffsll((unsigned long long)msk) - 1);
+            best = mx;
+        }
+        if (best >= cap) break;
+    }
+    return best >= kMinL ? m_pack(best, x - bestx) : 0u;
+}
+
+// stage block bytes [dbase, dbase + kLazyWindow) into dw (zero padded)
+__device__ void load_window(uint32_t *dw, const uint8_t *d, uint32_t dbase, uint32_t blen) {
+    const uint32_t lane = lane_id();
+    const uint32_t nload = min(kLazyWindow, blen - dbase);
+    const uint8_t *src = d + dbase;
+    if ((((uintptr_t)src) & 3) == 0) {
+        const uint32_t *src4 = (const uint32_t *)src;
+        const uint32_t nfull = nload >> 2;
+        for (uint32_t x = lane; x < kLazyWindow / 4 + 4; x += 64) {
+            uint32_t v = 0;
+            if (x < nfull) v = src4[x];
+            else if (x == nfull)
+                for (uint32_t q = 0; q < (nload & 3); q++) v |= (uint32_t)src[4 * x + q] << (8 * q);
+            dw[x] = v;
+        }
+    } else {
+        for (uint32_t x = lane; x < kLazyWindow / 4 + 4; x += 64) {
+            uint32_t v = 0;
+            for (uint32_t q = 0; q < 4; q++)
+                if (4 * x + q < nload) v |= (uint32_t)src[4 * x + q] << (8 * q);
+            dw[x] = v;
+        }
+    }
+}
+
+// set bit `setb` (if < 4096) and clear bits [lo, hi) of an LDS bitmap, lane-parallel
+__device__ inline void bm_apply(uint64_t *bm, uint32_t setb, uint32_t lo, uint32_t hi) {
+    const uint32_t lane = lane_id();
+    uint32_t first = 0xFFFFFFFFu, last = 0;
+    if (setb != 0xFFFFFFFFu) { first = setb; last = setb; }
+    if (hi > lo) { first = min(first, lo); last = max(last, hi - 1); }
+    if (first == 0xFFFFFFFFu) return;
+    const uint32_t wlo = first >> 6, whi = last >> 6;
+    for (uint32_t w = wlo + lane; w <= whi; w += 64) {
+        uint64_t v = bm[w];
+        const uint32_t a = max(lo, w * 64), z = min(hi, w * 64 + 64);
+        if (z > a) {
+            const uint32_t n = z - a;
+            const uint64_t msk = (n == 64 ? ~0ull : ((1ull << n) - 1)) << (a - w * 64);
+            v &= ~msk;
+        }
+        if (setb != 0xFFFFFFFFu && (setb >> 6) == w) v |= 1ull << (setb & 63);
+        bm[w] = v;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
+                                               uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_exit,
+                                               const uint32_t *__restrict__ tile_flags, BlockInfo *__restrict__ binfo) {
+    __shared__ uint32_t mL[kTile];
+    __shared__ uint64_t bmL[kTile / 64];
+    __shared__ uint32_t dw[kLazyWindow / 4 + 4];
+
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint64_t bstart = (uint64_t)b * L.B;
+    const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
+    const uint8_t *d = in + bstart;
+    const uint32_t ntiles = (blen + kTile - 1) / kTile;
+    uint32_t e = 0, dbase = 0xFFFFFFFFu, nlazy = 0, lazy_tiles = 0;
+
+    for (uint32_t k = 0; k < ntiles; k++) {
+        const uint32_t t0 = k * kTile, t1 = min(blen, t0 + kTile);
+        const uint32_t tix = b * L.tpb + k;
+        const bool lazy = (tile_flags[tix] & kTileLazy) != 0;
+        uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
+        const uint32_t nw = (t1 - t0 + 63) / 64;
+        if (e >= t1) {  // a match spans the whole tile
+            for (uint32_t w = lane; w < nw; w += 64) cw[w] = 0;
+            continue;
+        }
+        if (!lazy) {
+            const uint32_t rel = e - t0;
+            const uint64_t word = cw[rel >> 6];
+            if ((word >> (rel & 63)) & 1ull) {  // converged at the entry
+                const uint32_t full = rel >> 6;
+                for (uint32_t w = lane; w < full; w += 64) cw[w] = 0;
+                if (lane == 0 && (rel & 63)) cw[full] = word & (~0ull << (rel & 63));
+                e = tile_exit[tix];
+                continue;
+            }
+        }
+        // ---- slow path ----
+        lazy_tiles += lazy ? 1 : 0;
+        for (uint32_t x = lane; x < t1 - t0; x += 64) mL[x] = m[bstart + t0 + x];
+        for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
+        __syncthreads();
+        if (e > t0) bm_apply(bmL, 0xFFFFFFFFu, 0, e - t0);
+        __syncthreads();
+        uint32_t t = e, exitv;
+        for (;;) {
+            const uint32_t rel = t - t0;
+            if (!lazy && ((bmL[rel >> 6] >> (rel & 63)) & 1ull)) { exitv = tile_exit[tix]; break; }
+            uint32_t mm = mL[rel];
+            if (mm == kUnknown) {
+                const uint32_t lo = t > kWin ? t - kWin : 0;
+                if (dbase == 0xFFFFFFFFu || lo < dbase || t + kMaxL + 8 > dbase + kLazyWindow) {
+                    __syncthreads();
+                    dbase = lo & ~3u;
+                    load_window(dw, d, dbase, blen);
+                    __syncthreads();
+                }
+                mm = lazy_match(dw, dbase, blen, t);
+                nlazy++;
+                if (lane == 0) m[bstart + t] = mm;
+            }
+            const uint32_t nt = t + m_len(mm) + 1;
+            bm_apply(bmL, rel, rel + 1, min(nt, t1) - t0);
+            __syncthreads();
+            t = nt;
+            if (t >= t1) { exitv = t; break; }
+        }
+        for (uint32_t w = lane; w < nw; w += 64) cw[w] = bmL[w];
+        __syncthreads();
+        e = exitv;
+    }
+    if (lane == 0) {
+        binfo[b].lazy_evals = nlazy;
+        binfo[b].lazy_tiles = lazy_tiles;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-thread slice of a tile: 16 positions = one quarter of a chain word
+struct Slice {
+    uint32_t s, bits;
+};
+__device__ inline Slice tile_slice(const uint64_t *chain, const Layout &L, uint32_t b, uint32_t k, uint32_t t0,
+                                   uint32_t t1, uint32_t tid) {
+    Slice sl;
+    sl.s = t0 + tid * 16;
+    sl.bits = 0;
+    if (sl.s < t1) {
+        const uint64_t w = chain[(uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2)];
+        sl.bits = (uint32_t)(w >> (16 * (tid & 3))) & 0xFFFFu;
+        const uint32_t valid = min(16u, t1 - sl.s);
+        if (valid < 16) sl.bits &= (1u << valid) - 1;
+    }
+    return sl;
+}
+
+// block-wide exclusive scan of 3 counters (256 threads); returns totals in tot
+__device__ inline void block_scan3(uint32_t v[3], uint32_t tot[3], uint32_t *sh /* >= 3*4 */) {
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    uint32_t inc[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) inc[q] = wave_incl_scan(v[q]);
+    if (lane == 63)
+        for (int q = 0; q < 3; q++) sh[q * 4 + wv] = inc[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        uint32_t pre = 0, all = 0;
+        for (uint32_t w = 0; w < 4; w++) {
+            const uint32_t x = sh[q * 4 + w];
+            if (w < wv) pre += x;
+            all += x;
+        }
+        v[q] = pre + inc[q] - v[q];
+        tot[q] = all;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_tile_count(Layout L, const uint32_t *__restrict__ m,
+                                                    const uint64_t *__restrict__ chain, uint32_t *__restrict__ tile_cnt) {
+    __shared__ uint32_t sh[12];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
+    const uint64_t bstart = (uint64_t)b * L.B;
+    const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
+    const uint32_t t0 = k * kTile;
+    if (t0 >= blen) return;
+    const uint32_t t1 = min(blen, t0 + kTile);
+    const Slice sl = tile_slice(chain, L, b, k, t0, t1, tid);
+    uint32_t v[3] = {(uint32_t)__builtin_popcount(sl.bits), 0, 0};
+    for (uint32_t bits = sl.bits; bits; bits &= bits - 1) {
+        const uint32_t L_ = m_len(m[bstart + sl.s + __builtin_ctz(bits)]);
+        if (L_) { v[1]++; v[2] += (L_ >> 2) + 3; }
+    }
+    uint32_t tot[3];
+    block_scan3(v, tot, sh);
+    if (tid == 0) {
+        tile_cnt[3 * blockIdx.x + 0] = tot[0];
+        tile_cnt[3 * blockIdx.x + 1] = tot[1];
+        tile_cnt[3 * blockIdx.x + 2] = tot[2];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_block_scan(Layout L, const uint32_t *__restrict__ tile_cnt,
+                                                    uint32_t *__restrict__ tile_off, BlockInfo *__restrict__ binfo) {
+    __shared__ uint32_t sh[12];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint64_t bstart = (uint64_t)b * L.B;
+    const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
+    const uint32_t ntiles = (blen + kTile - 1) / kTile;
+    uint32_t carry[3] = {0, 0, 0};
+    for (uint32_t k0 = 0; k0 < ntiles; k0 += 256) {
+        const uint32_t k = k0 + tid;
+        uint32_t v[3] = {0, 0, 0};
+        if (k < ntiles)
+            for (int q = 0; q < 3; q++) v[q] = tile_cnt[3 * (b * L.tpb + k) + q];
+        uint32_t tot[3];
+        block_scan3(v, tot, sh);
+        if (k < ntiles)
+            for (int q = 0; q < 3; q++) tile_off[3 * (b * L.tpb + k) + q] = carry[q] + v[q];
+        for (int q = 0; q < 3; q++) carry[q] += tot[q];
+    }
+    if (tid == 0) {
+        BlockInfo &bi = binfo[b];
+        bi.len = blen;
+        bi.ntok = carry[0];
+        bi.nmatch = carry[1];
+        bi.gbits = carry[2];
+        bi.slen[0] = (carry[0] + 7) / 8;                 // flags bytes (2078-2079)
+        bi.slen[1] = carry[0];                           // chars
+        bi.slen[2] = (kPBits * carry[1]) / 8 + 1;        // (11*pCnt)/8 + 1 (2192)
+        bi.slen[3] = 4 * ((carry[2] + 31) / 32);         // golomb words as bytes
+    }
+}
+
+// LDS staging capacities per tile (words)
+constexpr uint32_t kFlagW = kTile / 32 + 2;
+constexpr uint32_t kPW = (kPBits * (kTile / 4)) / 32 + 3;
+constexpr uint32_t kGW = 128;
+
+__device__ inline void or_bits_lds(uint32_t *w, uint32_t wbase, uint64_t pos, uint32_t val, uint32_t nbits) {
+    // OR nbits (<= 32) of val at absolute bit pos into staged words (word index relative to wbase)
+    const uint32_t wi = (uint32_t)(pos >> 5) - wbase, sh = (uint32_t)(pos & 31);
+    atomicOr(&w[wi], val << sh);
+    if (sh + nbits > 32) atomicOr(&w[wi + 1], val >> (32 - sh));
+}
+
+__global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
+                                              const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_cnt,
+                                              const uint32_t *__restrict__ tile_off, uint8_t *__restrict__ s_flags,
+                                              uint8_t *__restrict__ s_chars, uint8_t *__restrict__ s_p,
+                                              uint8_t *__restrict__ s_golomb) {
+    __shared__ uint32_t sh[12];
+    __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
+    const uint64_t bstart = (uint64_t)b * L.B;
+    const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
+    const uint32_t t0 = k * kTile;
+    if (t0 >= blen) return;
+    const uint32_t t1 = min(blen, t0 + kTile);
+    const Slice sl = tile_slice(chain, L, b, k, t0, t1, tid);
+
+    uint32_t v[3] = {(uint32_t)__builtin_popcount(sl.bits), 0, 0};
+    for (uint32_t bits = sl.bits; bits; bits &= bits - 1) {
+        const uint32_t L_ = m_len(m[bstart + sl.s + __builtin_ctz(bits)]);
+        if (L_) { v[1]++; v[2] += (L_ >> 2) + 3; }
+    }
+    uint32_t tot[3];
+    block_scan3(v, tot, sh);
+    const uint32_t tix = blockIdx.x;
+    const uint32_t tok0 = tile_off[3 * tix + 0], mi0 = tile_off[3 * tix + 1], g0 = tile_off[3 * tix + 2];
+    uint32_t tok = tok0 + v[0], mi = mi0 + v[1], goff = g0 + v[2];
+    const uint32_t fw0 = tok0 >> 5, pw0 = (uint32_t)(((uint64_t)kPBits * mi0) >> 5), gw0 = g0 >> 5;
+    const uint32_t nfw = tot[0] ? ((tok0 + tot[0] - 1) >> 5) - fw0 + 1 : 0;
+    const uint32_t npw = tot[1] ? (uint32_t)(((uint64_t)kPBits * (mi0 + tot[1]) - 1) >> 5) - pw0 + 1 : 0;
+    const uint32_t ngw = tot[2] ? ((g0 + tot[2] - 1) >> 5) - gw0 + 1 : 0;
+    for (uint32_t w = tid; w < kFlagW; w += 256) lf[w] = 0;
+    for (uint32_t w = tid; w < kPW; w += 256) lp[w] = 0;
+    for (uint32_t w = tid; w < kGW; w += 256) lg[w] = 0;
+    __syncthreads();
+
+    const uint8_t *d = in + bstart;
+    uint8_t *chars = s_chars + (uint64_t)b * L.sstride[1];
+    for (uint32_t bits = sl.bits; bits; bits &= bits - 1) {
+        const uint32_t i = sl.s + __builtin_ctz(bits);
+        const uint32_t mm = m[bstart + i];
+        const uint32_t Lm = m_len(mm);
+        chars[tok] = d[i + Lm];
+        if (Lm == 0) {
+            atomicOr(&lf[(tok >> 5) - fw0], 1u << (tok & 31));
+        } else {
+            or_bits_lds(lp, pw0, (uint64_t)kPBits * mi, m_dist(mm), kPBits);
+            const uint32_t q = Lm >> 2, r = Lm & 3;
+            // q one-bits, a zero bit, then r (2 bits, LSB first)
+            uint32_t pos = goff, left = q;
+            while (left) {
+                const uint32_t sh_ = pos & 31, n = min(left, 32 - sh_);
+                const uint32_t msk = (n == 32 ? ~0u : ((1u << n) - 1)) << sh_;
+                atomicOr(&lg[(pos >> 5) - gw0], msk);
+                pos += n;
+                left -= n;
+            }
+            pos += 1;
+            if (r) or_bits_lds(lg, gw0, pos, r, 2);
+            mi++;
+            goff += q + 3;
+        }
+        tok++;
+    }
+    __syncthreads();
+    uint32_t *fw = (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]);
+    uint32_t *pw = (uint32_t *)(s_p + (uint64_t)b * L.sstride[2]);
+    uint32_t *gw = (uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]);
+    for (uint32_t w = tid; w < nfw; w += 256) if (lf[w]) atomicOr(&fw[fw0 + w], lf[w]);
+    for (uint32_t w = tid; w < npw; w += 256) if (lp[w]) atomicOr(&pw[pw0 + w], lp[w]);
+    for (uint32_t w = tid; w < ngw; w += 256) if (lg[w]) atomicOr(&gw[gw0 + w], lg[w]);
+}
+
+void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint32_t *tile_exit,
+                  uint32_t *tile_flags, uint32_t *tile_cnt, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags,
+                  uint8_t *s_chars, uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, int stage,
+                  hipEvent_t *ev) {
+    (void)stage; (void)ev;
+    const uint32_t ntiles = L.nblocks * L.tpb;
+    hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, chain, tile_exit, tile_flags, binfo);
+    if (ev) (void)hipEventRecord(ev[0], st);
+    hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(256), 0, st, L, m, chain, tile_cnt);
+    if (ev) (void)hipEventRecord(ev[1], st);
+    hipLaunchKernelGGL(k_block_scan, dim3(L.nblocks), dim3(256), 0, st, L, tile_cnt, tile_off, binfo);
+    if (ev) (void)hipEventRecord(ev[2], st);
+    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, chain, tile_cnt, tile_off, s_flags, s_chars,
+                       s_p, s_golomb);
+    if (ev) (void)hipEventRecord(ev[3], st);
+}
+
+}  // namespace fcx

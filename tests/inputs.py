@@ -1,0 +1,155 @@
+"""Deterministic test inputs, shared by the tests, the
+golden-vector script and smoke().
+
+Every input is described by a small JSON-able spec and re-created by `make(spec)`
+from tools/libfcxgen.so (glibc TYPE_3 rand embedded), so the committed fixtures
+carry data specs + expected outputs, never bulk bytes.
+"""
+import ctypes
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GEN_KIND = {"rand": 0, "zeros": 1, "runs": 2, "text": 3}
+MiB = 1 << 20
+
+_gen = None
+
+
+def gen_lib():
+    global _gen
+    if _gen is None:
+        _gen = ctypes.CDLL(os.path.join(ROOT, "tools", "libfcxgen.so"))
+        _gen.fcxgen_generate.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+        _gen.fcxgen_create.argtypes = [ctypes.c_int, ctypes.c_uint32]
+        _gen.fcxgen_create.restype = ctypes.c_void_p
+        _gen.fcxgen_fill.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        _gen.fcxgen_destroy.argtypes = [ctypes.c_void_p]
+        _gen.fcxgen_rand_values.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
+    return _gen
+
+
+def generate(kind: str, seed: int, n: int) -> bytes:
+    buf = ctypes.create_string_buffer(max(n, 1))
+    gen_lib().fcxgen_generate(GEN_KIND[kind], seed, buf, n)
+    return buf.raw[:n]
+
+
+def generate_into(kind: str, seed: int, ptr: int, n: int) -> None:
+    """fill host memory at `ptr` (e.g. a pinned torch tensor) with n bytes"""
+    gen_lib().fcxgen_generate(GEN_KIND[kind], seed, ctypes.c_void_p(ptr), n)
+
+
+def _lcg(seed):
+    x = seed & 0xFFFFFFFF
+    while True:
+        x = (1103515245 * x + 12345) & 0x7FFFFFFF
+        yield x
+
+
+def mosaic(seed: int, n: int) -> bytes:
+    """concatenation of pieces of every kind and many lengths: sparse/dense
+    transitions inside blocks and tiles (long zero runs inside text, periodic
+    stretches, random bursts)."""
+    r = _lcg(seed)
+    out = bytearray()
+    kinds = ["text", "rand", "runs", "zeros", "period", "text", "runs"]
+    while len(out) < n:
+        k = kinds[next(r) % len(kinds)]
+        ln = 1 + next(r) % 9000
+        if k == "period":
+            per = 1 + next(r) % 9
+            pat = generate("rand", next(r), per)
+            piece = (pat * (ln // per + 1))[:ln]
+        else:
+            piece = generate(k, next(r) % 1000 + 1, ln)
+        out += piece
+    return bytes(out[:n])
+
+
+def make(spec) -> bytes:
+    t = spec["type"]
+    if t == "tiny":          # bytes (7i+3) mod 256
+        return bytes((7 * i + 3) % 256 for i in range(spec["n"]))
+    if t == "seq":
+        return bytes(range(spec["n"]))
+    if t == "repeat":
+        return bytes.fromhex(spec["hex"]) * spec["count"]
+    if t == "gen":
+        return generate(spec["kind"], spec["seed"], spec["n"])
+    if t == "mosaic":
+        return mosaic(spec["seed"], spec["n"])
+    if t == "concat":
+        return b"".join(make(s) for s in spec["parts"])
+    raise ValueError(t)
+
+
+def _g(kind, seed, n, block, name=None):
+    return {"name": name or f"{kind}_s{seed}_{n}_b{block}", "type": "gen", "kind": kind,
+            "seed": seed, "n": n, "block": block}
+
+
+def golden_specs():
+    S = []
+    for n in [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 16, 17, 31, 64, 258, 259, 262, 1000]:
+        S.append({"name": f"tiny_{n}", "type": "tiny", "n": n, "block": MiB})
+    S.append({"name": "seq16", "type": "seq", "n": 16, "block": MiB})
+    S.append({"name": "seq256x40", "type": "repeat", "hex": bytes(range(256)).hex(), "count": 40, "block": MiB})
+    S.append({"name": "abcabd_x1000", "type": "repeat", "hex": b"abcabcabcabd".hex(), "count": 1000, "block": MiB})
+    S.append({"name": "A_x100000", "type": "repeat", "hex": b"A".hex(), "count": 100000, "block": MiB})
+    S.append({"name": "kat30", "type": "repeat", "hex": b"aacaacabcabaaacbaaacccaacabcad".hex(), "count": 1, "block": MiB})
+    for per in [1, 2, 3, 5, 8, 13]:
+        S.append({"name": f"period{per}", "type": "repeat", "hex": bytes((37 * i + 11) % 251 for i in range(per)).hex(),
+                  "count": 70000 // per, "block": 65536})
+    for kind, seed in [("rand", 1), ("text", 1), ("runs", 1), ("zeros", 0)]:
+        for block in [MiB, 65536, 262144]:
+            S.append(_g(kind, seed, MiB, block))
+    S.append(_g("text", 7, 300000, 4096))
+    S.append(_g("rand", 8, 100000, 1000))
+    S.append(_g("runs", 9, 200000, 10000))
+    S.append(_g("text", 11, 77777, 65536))
+    S.append(_g("zeros", 0, 5000, 1000))
+    for seed in [1, 2, 3]:
+        for block in [65536, MiB]:
+            S.append({"name": f"mosaic_s{seed}_b{block}", "type": "mosaic", "seed": seed, "n": 600000, "block": block})
+    S.append({"name": "text_zeros_text", "type": "concat", "block": MiB, "parts": [
+        {"type": "gen", "kind": "text", "seed": 21, "n": 100000},
+        {"type": "gen", "kind": "zeros", "seed": 0, "n": 50000},
+        {"type": "gen", "kind": "text", "seed": 22, "n": 100000}]})
+    S.append({"name": "text_plus_partial", "type": "concat", "block": 262144, "parts": [
+        {"type": "gen", "kind": "text", "seed": 5, "n": MiB + 12345}]})
+    return S
+
+
+def token_specs():
+    return [
+        {"name": "kat30", "type": "repeat", "hex": b"aacaacabcabaaacbaaacccaacabcad".hex(), "count": 1},
+        {"name": "abc300", "type": "repeat", "hex": b"abc".hex(), "count": 100},
+        {"name": "text5000", "type": "gen", "kind": "text", "seed": 3, "n": 5000},
+        {"name": "runs3000", "type": "gen", "kind": "runs", "seed": 4, "n": 3000},
+        {"name": "mosaic20000", "type": "mosaic", "seed": 9, "n": 20000},
+    ]
+
+
+# Digests of the reference's output on the full-size configs (SURVEY.md §8(c),
+# Appendix B.4): produced by the survey with the same in-place reference build
+# (8 processes over block ranges, byte-identical to the CLI).
+SURVEY_DIGESTS = {
+    "cfg2_rand_64MiB": {"kind": "rand", "seed": 2, "n": 64 * MiB, "block": 65536,
+                        "in": "d0ea0741abb3435057409137cdc79331b78c64ab0c5cbe8678e6fae40d3179cf",
+                        "bytes": 68819158, "out": "3b6853f2cf570b7a35c469efff62c15e0290b04ede45f6b47a97afc82c1878a5"},
+    "cfg3_text_1GiB": {"kind": "text", "seed": 3, "n": 1024 * MiB, "block": 262144,
+                       "in": "713e4aa36f5d3604cc756c4abf995bc0355d1c7387379c60bcd24b8556c3bdea",
+                       "bytes": 630008807, "out": "20219e60c2e9aef6659801fbfc53c6873ec811686eedcb45c0896fc5547d63d0"},
+    "cfg5a_zeros_1GiB": {"kind": "zeros", "seed": 0, "n": 1024 * MiB, "block": MiB,
+                         "in": "49bc20df15e412a64472421e13fe86ff1c5165e18b2afccf160d4dc19fe68a14",
+                         "bytes": 7521290, "out": "533fd45fbaa861a6060e9a5beac177cc0b64db691fc602a1e0e1e188afa5f912"},
+    "cfg5b_runs_1GiB": {"kind": "runs", "seed": 5, "n": 1024 * MiB, "block": MiB,
+                        "in": "18cddd87a89e44af896056a31ae955c56deea5bf47ab1de5ab491796d5115ef3",
+                        "bytes": 42548682, "out": "4fced94fd4725ba3b1031dec67d63e1295b95ae08cc1cf0e34c84769f5313d26"},
+    "hl_text_1GiB": {"kind": "text", "seed": 3, "n": 1024 * MiB, "block": MiB,
+                     "in": "713e4aa36f5d3604cc756c4abf995bc0355d1c7387379c60bcd24b8556c3bdea",
+                     "bytes": 624801500, "out": "132a36b9d2592f8c37a82b51f545ddb67acec53fa1a31b7f1f6a04617a01a3d1"},
+    "hl_rand_1GiB": {"kind": "rand", "seed": 4, "n": 1024 * MiB, "block": MiB,
+                     "in": "2a96181ea4cf7c0c9cfff49677640efe0a5a0b12ee5d0379f2bdf06d9c41f29d",
+                     "bytes": 1091294206, "out": "ee962534628bf6b2f79c51a44a65ac0845945e2fe9225e5be8f99f288912a69d"},
+}

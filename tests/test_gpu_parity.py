@@ -1,0 +1,148 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's own
+outputs (golden.json, made by the reference compiled in place) and against the
+oracle on seeded inputs.  Integer/byte work: the bar is bit-exact.
+
+Full-size configurations (BASELINE.json configs 2-5) are checked against the
+SHA-256 digests of the reference's output; at those sizes the
+oracle is not run, the digest is the size-independent check.
+"""
+import hashlib
+import os
+import random
+
+import pytest
+
+import inputs
+import my_compress_amd as mc
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu_compress(cuda):
+    import torch
+
+    ctxs = {}
+
+    def run(data: bytes, block: int) -> bytes:
+        if block not in ctxs:
+            ctxs[block] = mc.Context(0, block, max(len(data), block))
+        ctx = ctxs[block]
+        if not data:
+            return mc.write_header(0, 0)
+        d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
+        cap = mc.shard_bound(len(data), block)
+        d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+        n = ctx.compress_shard(d_in.data_ptr(), len(data), d_out.data_ptr(), cap,
+                               torch.cuda.current_stream().cuda_stream)
+        nb = (len(data) + block - 1) // block
+        return mc.write_header(len(data), nb) + d_out[:n].cpu().numpy().tobytes()
+
+    yield run
+    for c in ctxs.values():
+        c.close()
+
+
+def _cases(golden):
+    return [c for c in golden["cases"]]
+
+
+def test_golden_cases_bit_exact(golden, gpu_compress):
+    bad = []
+    for case in _cases(golden):
+        data = inputs.make(case)
+        assert hashlib.sha256(data).hexdigest() == case["in_sha256"], case["name"]
+        out = gpu_compress(data, case["block"])
+        if hashlib.sha256(out).hexdigest() != case["out_sha256"]:
+            bad.append((case["name"], len(out), case["out_bytes"]))
+    assert not bad, f"GPU output differs from the reference on {bad}"
+
+
+def test_small_hex_fixtures(golden, gpu_compress):
+    for case in _cases(golden):
+        if "out_hex" in case:
+            assert gpu_compress(inputs.make(case), case["block"]).hex() == case["out_hex"], case["name"]
+
+
+def test_block_api_matches_reference(golden):
+    """fcx_compress_block: the per-block drop-in for my_compress_file_lz77 (:2115)"""
+    import struct
+
+    for case in _cases(golden):
+        if "out_hex" not in case or case["in_bytes"] > case["block"]:
+            continue
+        data = inputs.make(case)
+        blob = bytes.fromhex(case["out_hex"])
+        (plen,) = struct.unpack_from("<I", blob, 10)
+        assert mc.my_compress_file_lz77(data) == blob[14:14 + plen], case["name"]
+
+
+def test_random_inputs_vs_oracle(gpu_compress):
+    rng = random.Random(1234)
+    for it in range(40):
+        n = rng.choice([1, 2, 3, 5, 17, 100, 1000, 4095, 4096, 4097, 8191, 12289, 70000, 200000, 333333])
+        block = rng.choice([1, 7, 64, 1000, 4096, 4097, 65536, 262144, 1 << 20])
+        if n // block > 4000:
+            block = 65536
+        data = inputs.mosaic(rng.randrange(1 << 30), n)
+        got = gpu_compress(data, block)
+        want = oracle.compress_file(data, block)
+        assert got == want, f"iteration {it}: n={n} block={block}"
+
+
+def test_dense_and_periodic_edges(gpu_compress):
+    # long matches capped at 257, matches crossing tile borders, cap shrinking at block end
+    cases = [
+        b"\x00" * 5000,
+        b"ab" * 40000,
+        (b"xyz" * 3000) + bytes(range(256)) * 10 + b"q" * 9000,
+        inputs.generate("runs", 77, 300000),
+        bytes(range(256)) * 300,
+        b"a" * 4097 + b"b" * 4095 + b"a" * 4096,
+    ]
+    for data in cases:
+        for block in [4096, 65536, 1 << 20]:
+            assert gpu_compress(data, block) == oracle.compress_file(data, block), (len(data), block)
+
+
+def test_round_trip_host_decoder(gpu_compress):
+    for kind, seed in [("rand", 3), ("text", 4), ("runs", 5)]:
+        data = inputs.generate(kind, seed, 3 << 20)
+        blob = gpu_compress(data, 1 << 20)
+        assert mc.decompress(blob) == data
+
+
+@pytest.mark.slow
+def test_cfg2_64MiB_rand_64KiB_digest(gpu_compress):
+    cfg = inputs.SURVEY_DIGESTS["cfg2_rand_64MiB"]
+    data = inputs.generate(cfg["kind"], cfg["seed"], cfg["n"])
+    assert hashlib.sha256(data).hexdigest() == cfg["in"]
+    out = gpu_compress(data, cfg["block"])
+    assert len(out) == cfg["bytes"]
+    assert hashlib.sha256(out).hexdigest() == cfg["out"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["hl_text_1GiB", "hl_rand_1GiB", "cfg3_text_1GiB", "cfg5a_zeros_1GiB",
+                                  "cfg5b_runs_1GiB"])
+def test_full_size_digests(name, cuda):
+    import torch
+
+    cfg = inputs.SURVEY_DIGESTS[name]
+    n, block = cfg["n"], cfg["block"]
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    inputs.generate_into(cfg["kind"], cfg["seed"], host.data_ptr(), n)
+    d_in = host.to(cuda)
+    cap = mc.shard_bound(n, block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+    ctx = mc.Context(0, block, n)
+    try:
+        got = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, torch.cuda.current_stream().cuda_stream)
+    finally:
+        ctx.close()
+    h = hashlib.sha256(mc.write_header(n, (n + block - 1) // block))
+    out_host = d_out[:got].cpu()
+    h.update(memoryview(out_host.numpy()))
+    assert got + 10 == cfg["bytes"]
+    assert h.hexdigest() == cfg["out"]

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Developer timing: compress a device-resident synthetic shard with per-stage
+hipEvent timing and (optionally) check the output digest against the
+reference's.
+
+    python tools/devbench.py --kind text --gib 1 --block 1048576 --check hl_text_1GiB
+"""
+import argparse
+import hashlib
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import torch  # noqa: E402
+
+import inputs  # noqa: E402
+import my_compress_amd as mc  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kind", default="rand")
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--mib", type=int, default=1024)
+    ap.add_argument("--block", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--check", default=None)
+    a = ap.parse_args()
+    n = a.mib << 20
+    t = time.time()
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    inputs.generate_into(a.kind, a.seed, host.data_ptr(), n)
+    print(f"gen {a.kind} {a.mib} MiB: {time.time() - t:.1f}s", flush=True)
+    dev = torch.device("cuda:0")
+    d_in = host.to(dev)
+    cap = mc.shard_bound(n, a.block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx = mc.Context(0, a.block, n)
+    st = torch.cuda.current_stream().cuda_stream
+    got = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)  # warm
+    ctx.set_profiling(True)
+    for r in range(a.reps):
+        torch.cuda.synchronize()
+        t = time.time()
+        got = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)
+        torch.cuda.synchronize()
+        dt = time.time() - t
+        print(f"rep {r}: {dt * 1e3:.2f} ms  {n / dt / 1e9:.2f} GB/s  out={got} ratio={got / n:.4f}", flush=True)
+    for name, ms in ctx.stage_times():
+        print(f"   {name:14s} {ms:9.3f} ms")
+    print(ctx.stats())
+    if a.check:
+        cfg = inputs.SURVEY_DIGESTS[a.check]
+        h = hashlib.sha256(mc.write_header(n, (n + a.block - 1) // a.block))
+        h.update(memoryview(d_out[:got].cpu().numpy()))
+        print("digest", "OK" if h.hexdigest() == cfg["out"] and got + 10 == cfg["bytes"] else "MISMATCH",
+              got + 10, cfg["bytes"])
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
