@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""bench.py — compress throughput of the MI355X FCX7 LZ77 + Huffman path.
+
+Metric (BASELINE.json): compress MB/s on 1 GB synthetic bytes at 1/2/4/8 MI355X;
+% HBM roofline.  One process per GPU (torchrun for N > 1).  A "step" compresses
+the rank's whole device-resident shard (1 GiB = 1024 x 1 MiB blocks by default)
+into [u32 len][payload]... in HBM.  Shards are independent block ranges, so the
+data path has no collective (scaling: weak); the RCCL all-gather that
+concatenates the per-rank segments is timed after the timed region as its own
+stage ("concat").
+
+Default workload: rand = glibc rand()%256 seed 4, rank r = bytes [r GiB,
+(r+1) GiB) of that one stream (BASELINE config 4 sharding; N=1 is SURVEY's
+HL-rand, whose output digest is checked).  The text leg (seed 3 + rank; N=1 is
+HL-text) is measured in the same run and reported under "text".
+
+    python bench.py                      # N=1, defaults
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "compress MB/s on 1 GB synthetic bytes at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HL_DIGEST = {  # reference output digests for the N=1 shards
+    ("rand", 4, 1 << 30, 1 << 20): ("ee962534628bf6b2f79c51a44a65ac0845945e2fe9225e5be8f99f288912a69d", 1091294206),
+    ("text", 3, 1 << 30, 1 << 20): ("132a36b9d2592f8c37a82b51f545ddb67acec53fa1a31b7f1f6a04617a01a3d1", 624801500),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_shard(kind, seed, rank, n):
+    """pinned host tensor with rank's shard of the synthetic stream"""
+    import torch
+
+    import inputs
+
+    G = inputs.gen_lib()
+    G.fcxgen_skip.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    if kind == "rand":
+        h = G.fcxgen_create(inputs.GEN_KIND["rand"], seed)
+        G.fcxgen_skip(h, rank * n)   # one stream, rank r starts at byte r*n
+        G.fcxgen_fill(h, host.data_ptr(), n)
+        G.fcxgen_destroy(h)
+    else:
+        inputs.generate_into(kind, seed + rank, host.data_ptr(), n)
+    return host
+
+
+def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages):
+    import torch
+
+    import my_compress_amd as mc
+
+    n = args.mib << 20
+    t = time.time()
+    host = make_shard(kind, seed, rank, n)
+    gen_s = time.time() - t
+    d_in = host.to(dev)
+    del host
+    cap = mc.shard_bound(n, args.block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx = mc.Context(dev.index, args.block, n)
+    stream = torch.cuda.current_stream(dev)
+    sid = stream.cuda_stream
+    out_len = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid)  # validates the call
+    for _ in range(args.warmup):
+        ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid, sync=False)
+    ctx.set_profiling(profile_stages)
+    stage_sum = {}
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid, sync=False)
+        if profile_stages:
+            for name, ms in ctx.stage_times():   # waits for this step's last event
+                stage_sum[name] = stage_sum.get(name, 0.0) + ms
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    out_len = ctx.read_out_len()   # segment size of the timed steps (device word)
+    res = {
+        "kind": kind, "bytes_per_gpu": n, "out_bytes": out_len, "ratio": out_len / n,
+        "seconds": dt, "ms_per_step": dt / args.steps * 1e3,
+        "value": world * n * args.steps / dt / 1e6, "gen_s": gen_s,
+        "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
+    }
+    stats = ctx.stats()
+    res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
+    res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
+    key = (kind, seed, n, args.block)
+    if rank == 0 and world == 1 and key in HL_DIGEST and not args.no_verify:
+        import my_compress_amd as mc2
+
+        h = hashlib.sha256(mc2.write_header(n, (n + args.block - 1) // args.block))
+        h.update(memoryview(d_out[:out_len].cpu().numpy()))
+        want_sha, want_bytes = HL_DIGEST[key]
+        res["bit_exact_vs_reference"] = h.hexdigest() == want_sha and out_len + 10 == want_bytes
+    concat = None
+    if dist and world > 1 and args.concat == "allgather":
+        concat = allgather_concat(d_out, out_len, world, dev, dist)
+    ctx.close()
+    del d_in, d_out
+    torch.cuda.empty_cache()
+    return res, concat
+
+
+def allgather_concat(d_out, seg_len, world, dev, dist):
+    """RCCL all-gather of the per-rank segments (sizes first, then segments padded
+    to the max), assembled in rank order on every rank."""
+    import torch
+
+    sizes = torch.tensor([seg_len], dtype=torch.int64, device=dev)
+    all_sizes = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    dist.all_gather_into_tensor(all_sizes, sizes)
+    szs = [int(x) for x in all_sizes.cpu()]
+    mx = max(szs)
+    recv = torch.empty(world * mx, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(recv, d_out[:mx])
+    whole = torch.cat([recv[r * mx: r * mx + szs[r]] for r in range(world)])
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    total = int(whole.numel())
+    del recv, whole
+    return {"kind": "allgather", "ms": dt * 1e3, "bytes": total, "GBps_per_rank_recv": (total - seg_len) / dt / 1e9}
+
+
+def cpu_baseline(kind, seed, block, threads=16, nblocks=32):
+    """the reference's block encoder (oracle/_ref, compiled from /root/reference) on
+    the first nblocks blocks of the same shard, `threads` host threads"""
+    import oracle
+
+    R = oracle.ref()
+    kind_used = "reference"
+    if R is None:
+        kind_used = "port"
+    import inputs
+
+    n = block * nblocks
+    data = inputs.generate(kind, seed, n)
+    blocks = [data[i:i + block] for i in range(0, n, block)]
+    lock = threading.Lock()
+    todo = list(range(len(blocks)))
+
+    def worker():
+        ob = ctypes.create_string_buffer(2 * block + 4096)
+        while True:
+            with lock:
+                if not todo:
+                    return
+                i = todo.pop()
+            if R is not None:
+                R.ref_compress_block(blocks[i], len(blocks[i]), ob)
+            else:
+                oracle.orc().orc_compress_block(blocks[i], len(blocks[i]), ob, oracle.FINDER_SUNDAY)
+
+    if R is not None:
+        R.ref_set_quiet(1)
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker) for _ in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    if R is not None:
+        R.ref_set_quiet(0)
+    return {"value": n / dt / 1e6, "unit": "MB/s", "cores": threads, "kind": kind_used,
+            "sample": f"first {nblocks} x {block // 1024} KiB blocks of the {kind} shard, {threads} threads "
+                      f"({'reference my_compress_file_lz77 compiled in place' if R is not None else 'oracle port'})",
+            "seconds": dt}
+
+
+def load_pmc(path):
+    if path and os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kind", default="rand", choices=["rand", "text", "runs", "zeros"])
+    ap.add_argument("--mib", type=int, default=1024, help="MiB per GPU")
+    ap.add_argument("--block", type=int, default=1 << 20)
+    ap.add_argument("--no-text", action="store_true", help="skip the text leg")
+    ap.add_argument("--concat", default="allgather", choices=["allgather", "none"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    args = ap.parse_args()
+
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_
+
+        dist_.init_process_group("nccl", device_id=dev)
+        dist = dist_
+    seeds = {"rand": 4, "text": 3, "runs": 5, "zeros": 0}
+    main_res, concat = run_leg(args.kind, seeds[args.kind], args, rank, world, dev, dist, True)
+    text_res = None
+    if not args.no_text and args.kind != "text":
+        text_res, _ = run_leg("text", 3, args, rank, world, dev, dist, True)
+
+    if rank == 0:
+        stages = {k: v for k, v in main_res["stages_ms"].items() if k != "memset"}
+        dom = max(stages, key=stages.get) if stages else None
+        n = main_res["bytes_per_gpu"]
+        alg = n + main_res["out_bytes"]          # 1 + r bytes per input byte
+        achieved = alg / (stages[dom] * 1e-3) / 1e9 if dom else None
+        pmc = load_pmc(args.pmc)
+        traffic = None
+        key = f"{args.kind}:{dom}"
+        if key in pmc:
+            traffic = pmc[key].get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "kernel": f"k_{dom}" if dom else None, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "alg_bytes_per_launch": alg,
+                "note": "algorithmic bytes = input + compressed output per launch (1 + r per input byte); "
+                        "the path is compare/serial-bound, HBM fraction is small by construction",
+                "path_achieved": alg / (main_res["ms_per_step"] * 1e-3) / 1e9}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.kind, seeds[args.kind], args.block)
+        line = {
+            "metric": METRIC, "value": main_res["value"], "unit": "MB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": main_res["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: glibc rand()%256 seed 4, rank r = bytes [r*shard, (r+1)*shard) of one stream "
+                    "(SURVEY.md §8(d)); text leg: SURVEY enwik-style generator, seed 3+rank",
+            "config": {"workload": f"{args.kind} {args.mib} MiB per GPU, {args.block // 1024} KiB blocks "
+                                   f"(BASELINE config 4 sharding; N=1 = HL-{args.kind})",
+                       "kind": args.kind, "bytes_per_gpu": n, "block_bytes": args.block,
+                       "global_bytes": n * world, "parallelism": f"block-sharded x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "ratio": main_res["ratio"],
+            "bit_exact_vs_reference": main_res.get("bit_exact_vs_reference"),
+            "stages_ms": main_res["stages_ms"],
+            "lazy_evals": main_res["lazy_evals"],
+            "concat": concat,
+        }
+        if text_res:
+            line["text"] = {k: text_res[k] for k in ["value", "ms_per_step", "ratio", "stages_ms", "lazy_evals"]}
+            line["text"]["bit_exact_vs_reference"] = text_res.get("bit_exact_vs_reference")
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

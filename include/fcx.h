@@ -86,6 +86,8 @@ int fcx_compress_shard(fcx_ctx *ctx, const uint8_t *d_in, uint64_t n, uint8_t *d
                        uint64_t *out_len, void *stream);
 /* device address of the u64 output length written by the last fcx_compress_shard */
 const uint64_t *fcx_ctx_device_out_len(fcx_ctx *ctx);
+/* waits for the device and reads that length (and the device error bits) */
+int fcx_ctx_read_out_len(fcx_ctx *ctx, uint64_t *out_len);
 
 /* Host-to-host convenience for the CLI: compresses host memory in shards of up
  * to the context's shard size (H2D, device pipeline, D2H) and writes the same

@@ -62,6 +62,7 @@ def lib():
                                      ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
     L.fcx_ctx_device_out_len.argtypes = [ctypes.c_void_p]
     L.fcx_ctx_device_out_len.restype = ctypes.c_void_p
+    L.fcx_ctx_read_out_len.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_compress_host.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p, ctypes.c_uint64,
                                     ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -119,6 +120,12 @@ class Context:
 
     def device_out_len_ptr(self) -> int:
         return int(lib().fcx_ctx_device_out_len(self._h))
+
+    def read_out_len(self) -> int:
+        """waits for the device; output bytes of the last compress_shard"""
+        out = ctypes.c_uint64(0)
+        _check(lib().fcx_ctx_read_out_len(self._h, ctypes.byref(out)), "fcx_ctx_read_out_len")
+        return out.value
 
     def compress_host(self, data: bytes) -> bytes:
         cap = shard_bound(len(data), self.block_bytes)

@@ -96,6 +96,7 @@ struct fcx_ctx {
     bool profiling = false;
     hipEvent_t ev[kNumStages + 1] = {};
     bool have_times = false;
+    bool timed = false;        // last call recorded events
     float ms[kNumStages] = {};
     Layout last{};
 };
@@ -223,16 +224,29 @@ void fcx_ctx_destroy(fcx_ctx *c) {
 
 const uint64_t *fcx_ctx_device_out_len(fcx_ctx *c) { return c ? c->dev_words : nullptr; }
 
+int fcx_ctx_read_out_len(fcx_ctx *c, uint64_t *out_len) {
+    if (!c || !out_len) return fail(FCX_ERR_ARG, "fcx_ctx_read_out_len: NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 16, hipMemcpyDeviceToHost));
+    const uint32_t e = (uint32_t)c->host_words[1];
+    if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
+    if (e) return fail(FCX_ERR_INTERNAL, "device invariant violated (error bits " + std::to_string(e) + ")");
+    *out_len = c->host_words[0];
+    return FCX_OK;
+}
+
 int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
     if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
     c->profiling = enable != 0;
     return FCX_OK;
 }
 
-int fcx_ctx_stage_count(fcx_ctx *c) { return c && c->have_times ? kNumStages : 0; }
+int fcx_ctx_stage_count(fcx_ctx *c) { return c && c->timed ? kNumStages : 0; }
 
 int fcx_ctx_stage(fcx_ctx *c, int i, const char **name, float *ms) {
     if (!c || i < 0 || i >= kNumStages) return fail(FCX_ERR_ARG, "bad stage");
+    if (!c->timed) return fail(FCX_ERR_ARG, "last call was not profiled");
     if (!c->have_times) {
         HIP_TRY(hipEventSynchronize(c->ev[kNumStages]));
         for (int k = 0; k < kNumStages; k++) HIP_TRY(hipEventElapsedTime(&c->ms[k], c->ev[k], c->ev[k + 1]));
@@ -261,6 +275,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     c->last = L;
     c->have_times = false;
     hipEvent_t *ev = c->profiling ? c->ev : nullptr;
+    c->timed = ev != nullptr;
     uint64_t *total = c->dev_words;
     uint32_t *err = (uint32_t *)(c->dev_words + 1);
 

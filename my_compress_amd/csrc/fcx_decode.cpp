@@ -125,7 +125,9 @@ extern "C" int64_t fcx_decompress_block(const uint8_t *in, uint32_t len, uint8_t
     uint32_t mi = 0;
     for (uint32_t t = 0; t < N; t++) {
         if (!((flags[t >> 3] >> (t & 7)) & 1)) {
-            if (mi >= pcnt) return FCX_ERR_FORMAT;
+            // the reference stops at the first match token it has no (p, l) for
+            // ("Fatal Error!!!", break at 2331-2335) and decodes the tokens before it
+            if (mi >= pcnt) break;
             const uint32_t p = dist[mi], L = mlen[mi++];
             if (p == 0 || p > o || o + L + 1 > cap) return FCX_ERR_FORMAT;
             for (uint32_t k = 0; k < L; k++, o++) out[o] = out[o - p];

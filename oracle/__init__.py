@@ -61,6 +61,7 @@ def ref():
         L.ref_compress_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p]
         L.ref_compress_block.restype = ctypes.c_uint32
         L.ref_set_quiet.argtypes = [ctypes.c_int]
+        L.ref_set_quiet(1)   # the reference printf()s per block (my_compress.cpp:2249)
         _ref = L
     return _ref
 

@@ -417,7 +417,7 @@ int64_t orc_decompress_block(const uint8_t *in, uint32_t len, uint8_t *out, uint
     for (uint32_t t = 0; t < N; t++) {
         int lit = (flags[t >> 3] >> (t & 7)) & 1;
         if (!lit) {
-            if (mi >= pc) goto done;
+            if (mi >= pc) break;   /* reference: "Fatal Error", stops building tokens (2331-2335) */
             uint32_t dist = p[mi], L = l[mi++];
             if (dist == 0 || dist > o || o + L + 1 > cap) goto done;
             for (uint32_t k = 0; k < L; k++, o++) out[o] = out[o - dist];

@@ -48,6 +48,7 @@ extern "C" uint32_t ref_compress_block(const uint8_t *in, uint32_t len, uint8_t 
     memcpy(buf, in, len);
     uInt8 *obuf = new uInt8[2 * (size_t)len + 4096]();
     uInt32 n = my_compress_file_lz77(buf, len, obuf);
+    fflush(stdout);  /* push the per-block printf (2249) to wherever fd 1 points now */
     memcpy(out, obuf, n);
     delete[] buf;
     delete[] obuf;

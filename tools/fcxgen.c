@@ -25,7 +25,7 @@
 /* ---- glibc random_r TYPE_3 (deg 31, sep 3) -------------------------------- */
 typedef struct {
     int32_t r[34];   /* ring of the last 34 outputs of the recurrence */
-    uint32_t k;      /* index of the next value in the full sequence */
+    uint32_t k;      /* ring slot (0..33) of the next value */
 } glibc_rand_t;
 
 static void grand_seed(glibc_rand_t *g, uint32_t seed) {
@@ -46,14 +46,15 @@ static void grand_seed(glibc_rand_t *g, uint32_t seed) {
     g->k = 0; /* next rand() returns r[344 + 0] >> 1 */
 }
 
-/* the k-th rand() returns r[344+k] >> 1; ring slot = (344+k) mod 34 handled by
- * keeping a sliding window of 34 raw values starting at index 344 + k. */
+/* the k-th rand() returns r[344+k] >> 1; the ring holds the 34 raw values
+ * r[344+k .. 344+k+34) and slot g->k holds r[344+k]. */
 static inline int32_t grand_next(glibc_rand_t *g) {
-    uint32_t k = g->k++;
-    uint32_t slot = k % 34u;
+    uint32_t slot = g->k;
+    g->k = slot == 33 ? 0 : slot + 1;
     int32_t v = g->r[slot];
     /* value for index 344+k+34 = r[344+k+3] + r[344+k+31] */
-    uint32_t s3 = (k + 3) % 34u, s31 = (k + 31) % 34u;
+    uint32_t s3 = slot + 3 >= 34 ? slot + 3 - 34 : slot + 3;
+    uint32_t s31 = slot + 31 >= 34 ? slot + 31 - 34 : slot + 31;
     g->r[slot] = (int32_t)((uint32_t)g->r[s3] + (uint32_t)g->r[s31]);
     return (int32_t)((uint32_t)v >> 1);
 }
@@ -163,6 +164,56 @@ void fcxgen_fill(void *h, uint8_t *out, uint64_t n) {
         }
         break;
     }
+}
+
+/* ---- jump-ahead for the rand kind ------------------------------------------
+ * r[i] = r[i-31] + r[i-3] (mod 2^32) is linear: with s = r[j..j+31) the state at
+ * the next output index j, one step maps s -> (s[1..30], s[0] + s[28]).  Skipping
+ * k outputs applies M^k (31x31 over Z/2^32) by binary powering: O(31^3 log k).
+ * Lets rank r of a multi-GPU run start at byte r*shard of one seeded stream
+ * (BASELINE config 4: 8 GiB rand seed 4 sharded over 8 GPUs).                 */
+typedef struct { uint32_t a[31][31]; } mat31;
+
+static void mat_mul(const mat31 *x, const mat31 *y, mat31 *z) {
+    for (int i = 0; i < 31; i++)
+        for (int j = 0; j < 31; j++) {
+            uint32_t acc = 0;
+            for (int k = 0; k < 31; k++) acc += x->a[i][k] * y->a[k][j];
+            z->a[i][j] = acc;
+        }
+}
+
+int fcxgen_skip(void *h, uint64_t k) {
+    fcxgen_t *s = (fcxgen_t *)h;
+    if (!s || s->kind != GEN_RAND) return -1;
+    uint32_t st[31], nst[31];
+    for (int i = 0; i < 31; i++) st[i] = (uint32_t)s->g.r[(s->g.k + i) % 34u];
+    mat31 base, res, tmp;
+    memset(&base, 0, sizeof(base));
+    for (int i = 0; i < 30; i++) base.a[i][i + 1] = 1;
+    base.a[30][0] = 1;
+    base.a[30][28] = 1;
+    memset(&res, 0, sizeof(res));
+    for (int i = 0; i < 31; i++) res.a[i][i] = 1;
+    uint64_t e = k;
+    while (e) {
+        if (e & 1) { mat_mul(&res, &base, &tmp); res = tmp; }
+        mat_mul(&base, &base, &tmp);
+        base = tmp;
+        e >>= 1;
+    }
+    for (int i = 0; i < 31; i++) {
+        uint32_t acc = 0;
+        for (int j = 0; j < 31; j++) acc += res.a[i][j] * st[j];
+        nst[i] = acc;
+    }
+    /* rebuild the 34-entry ring for the new position */
+    s->g.k = (uint32_t)((s->g.k + k) % 34u);
+    uint32_t vals[34];
+    for (int i = 0; i < 31; i++) vals[i] = nst[i];
+    for (int i = 31; i < 34; i++) vals[i] = vals[i - 31] + vals[i - 3];
+    for (int i = 0; i < 34; i++) s->g.r[(s->g.k + i) % 34u] = (int32_t)vals[i];
+    return 0;
 }
 
 /* one-shot convenience: n bytes of `kind` with `seed` */
