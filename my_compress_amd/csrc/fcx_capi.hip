@@ -13,11 +13,11 @@
 #include "fcx_device.h"
 
 namespace fcx {
-void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint32_t *tile_exit,
-                  uint32_t *tile_flags, hipStream_t st);
-void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint32_t *tile_exit,
-                  uint32_t *tile_flags, uint32_t *tile_cnt, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags,
-                  uint8_t *s_chars, uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, int stage, hipEvent_t *ev);
+void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint64_t *chain_pfx,
+                  uint32_t *tinfo, hipStream_t st);
+void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, const uint64_t *chain_pfx,
+                  const uint32_t *tinfo, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
+                  uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev);
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
                     uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_bits,
                     uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
@@ -46,9 +46,9 @@ int hip_fail(hipError_t e, const char *what) {
 
 inline uint32_t round16(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
 
-const char *kStageNames[] = {"memset",  "match", "stitch",       "tile_count",  "block_scan", "emit",   "hist",
-                             "tree",    "bitcount", "block_layout", "scan_blocks", "zero",       "encode", "headers"};
-constexpr int kNumStages = 14;
+const char *kStageNames[] = {"memset", "match",        "stitch",      "emit", "hist",   "tree",
+                             "bitcount", "block_layout", "scan_blocks", "zero", "encode", "headers"};
+constexpr int kNumStages = 12;
 
 Layout make_layout(uint64_t n, uint32_t B) {
     Layout L;
@@ -80,7 +80,9 @@ struct fcx_ctx {
     // scratch (device)
     uint32_t *m = nullptr;
     uint64_t *chain = nullptr;
-    uint32_t *tile_exit = nullptr, *tile_flags = nullptr, *tile_cnt = nullptr, *tile_off = nullptr;
+    uint64_t *chain_pfx = nullptr;     // per 64 positions: speculative prefix counts (k_match)
+    uint32_t *tinfo = nullptr;         // per tile: flags, exit, token/match/golomb-bit totals
+    uint32_t *tile_off = nullptr;      // per tile: token/match/golomb-bit offsets (k_stitch)
     BlockInfo *binfo = nullptr;
     uint8_t *s[kStreams] = {nullptr, nullptr, nullptr, nullptr};
     uint32_t *hist = nullptr, *ctab = nullptr, *chunk_bits = nullptr;
@@ -103,12 +105,12 @@ struct fcx_ctx {
 
 namespace {
 void free_scratch(fcx_ctx *c) {
-    void *ptrs[] = {c->m,    c->chain, c->tile_exit, c->tile_flags, c->tile_cnt, c->tile_off, c->binfo,
+    void *ptrs[] = {c->m,    c->chain, c->chain_pfx, c->tinfo,      c->tile_off, c->binfo,
                     c->s[0], c->s[1],  c->s[2],      c->s[3],       c->hist,     c->ctab,     c->chunk_bits,
                     c->ltab, c->hhdr,  c->blk_off};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    c->m = nullptr; c->chain = nullptr; c->tile_exit = c->tile_flags = c->tile_cnt = c->tile_off = nullptr;
+    c->m = nullptr; c->chain = c->chain_pfx = nullptr; c->tinfo = c->tile_off = nullptr;
     c->binfo = nullptr;
     for (auto &p : c->s) p = nullptr;
     c->hist = c->ctab = c->chunk_bits = nullptr;
@@ -133,9 +135,8 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     int r;
     if ((r = dalloc(&c->m, 4ull * nb * c->B, "m"))) return r;
     if ((r = dalloc(&c->chain, 8ull * nb * L.wpb, "chain"))) return r;
-    if ((r = dalloc(&c->tile_exit, 4 * nt, "tile_exit"))) return r;
-    if ((r = dalloc(&c->tile_flags, 4 * nt, "tile_flags"))) return r;
-    if ((r = dalloc(&c->tile_cnt, 12 * nt, "tile_cnt"))) return r;
+    if ((r = dalloc(&c->chain_pfx, 8ull * (kTile / 64) * nt, "chain_pfx"))) return r;
+    if ((r = dalloc(&c->tinfo, 32 * nt, "tinfo"))) return r;
     if ((r = dalloc(&c->tile_off, 12 * nt, "tile_off"))) return r;
     if ((r = dalloc(&c->binfo, sizeof(BlockInfo) * nb, "binfo"))) return r;
     for (uint32_t s = 0; s < kStreams; s++)
@@ -286,12 +287,12 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     HIP_TRY(hipMemsetAsync(c->s[3], 0, (uint64_t)L.sstride[3] * L.nblocks, st));
     HIP_TRY(hipMemsetAsync(c->hist, 0, 4ull * 256 * kStreams * L.nblocks, st));
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
-    launch_match(d_in, L, c->m, c->chain, c->tile_exit, c->tile_flags, st);
+    launch_match(d_in, L, c->m, c->chain, c->chain_pfx, c->tinfo, st);
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
-    launch_parse(d_in, L, c->m, c->chain, c->tile_exit, c->tile_flags, c->tile_cnt, c->tile_off, c->binfo, c->s[0],
-                 c->s[1], c->s[2], c->s[3], st, 0, ev ? ev + 3 : nullptr);
+    launch_parse(d_in, L, c->m, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->binfo, c->s[0], c->s[1], c->s[2],
+                 c->s[3], st, ev ? ev + 3 : nullptr);
     launch_entropy(L, c->binfo, c->s[0], c->s[1], c->s[2], c->s[3], c->hist, c->ctab, c->ltab, c->hhdr,
-                   c->chunk_bits, c->blk_off, total, d_out, cap, err, st, ev ? ev + 7 : nullptr);
+                   c->chunk_bits, c->blk_off, total, d_out, cap, err, st, ev ? ev + 5 : nullptr);
     HIP_TRY(hipGetLastError());
     if (out_len) {
         HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 16, hipMemcpyDeviceToHost, st));

@@ -14,8 +14,8 @@ constexpr uint32_t kPBits = 11;     // P_BITS
 
 // ---- device work decomposition --------------------------------------------
 constexpr uint32_t kTile = 4096;            // positions per match-kernel workgroup
-constexpr uint32_t kMatchThreads = 256;
-constexpr uint32_t kSubSeg = kTile / kMatchThreads;  // 16 positions per lane in the tile parse
+constexpr uint32_t kMatchThreads = 512;
+constexpr uint32_t kSubSeg = kTile / kMatchThreads;  // 8 positions per lane in the tile parse
 constexpr uint32_t kHashBits = 12;
 constexpr uint32_t kHalo = kWin;                     // left halo of a tile
 constexpr uint32_t kLookAhead = 260;                 // right look-ahead bytes (>= 257)

@@ -4,44 +4,58 @@
 // longest_match_sunday (1446-1514) driven by Sunday_Search (1407-1443).  The
 // reference's result at cursor i is the LEFTMOST j in [max(0,i-2047), i) with the
 // MAXIMUM common prefix L, L capped at min(258, len-i)-1, literal if L < 3
-// (SURVEY.md §0 finding 3).  Here one 256-lane workgroup owns a tile of 4096
+// (SURVEY.md §0 finding 3).  One 512-lane workgroup owns a tile of 4096
 // positions of one block:
 //
-//   1. stage [t0-2048, t1+260) of the block in LDS (coalesced, dword loads);
-//   2. insert every window position into a 4096-bucket hash table of 3-byte keys,
-//      in 256-position passes separated by barriers, so a chain runs newest pass
-//      first; query the pass's tile positions right after it is inserted — a
-//      chain walk then meets exactly the window candidates, and stops as soon as
-//      it reaches a pass lying wholly below i-2047;
-//   3. exact max-length / min-position selection over the key-equal candidates
-//      (dword compares in LDS); a position whose window holds more than
-//      kMaxChainSteps candidates is left "unknown" for the stitch kernel's
+//   1. stage [t0-2048, t1+260) of the block in LDS (dword loads);
+//   2. insert every window position into a 4096-bucket table of 3-byte keys.  The
+//      key is split by a bijection of Z/2^24 into (12-bit bucket, 12-bit tag), so
+//      a chain node {tag, next} identifies the key exactly and a chain step is one
+//      LDS read;
+//   3. every tile position walks its bucket (order irrelevant: all entries are
+//      visited) and keeps the max-length / min-position candidate among those in
+//      its window.  The walk is latency-bound, so each lane runs four walks
+//      interleaved; a candidate's length is read off two dword compares against
+//      the query's preloaded bytes 3..10, and only a match reaching 11 bytes
+//      enters the byte-by-dword extension loop.  A position seeing more than
+//      kMaxChainSteps entries is left "unknown" for the stitch kernel's
 //      wave-parallel evaluation (runs / zeros: long matches, few tokens);
 //   4. greedy parse of the tile assuming a token starts at t0: each lane walks
-//      its 16 positions, then lanes agree on sub-segment entry points by a
-//      Jacobi fixed point (entry_k+1 = exit of walking sub-segment k from entry_k)
-//      that converges in a few rounds because greedy chains resynchronise.
-//
-// Outputs: m[i] for every position, the tile's chain bitmap (positions that start
-// a token if a token starts at t0), and the tile's exit (first chain position
-// >= t1).  Tiles with unknown positions are flagged lazy.
+//      its 8 positions, lanes agree on sub-segment entries by a Jacobi fixed
+//      point (entry_{k+1} = exit of sub-segment k walked from entry_k) that
+//      converges in one or two rounds because greedy chains resynchronise; then
+//      the tile's chain bitmap, per-64-position prefix counts (tokens, matches,
+//      golomb bits) and totals are published for the stitch kernel.
+#include <cstdlib>
+
 #include "fcx_device.h"
 
 namespace fcx {
 
-__global__ __launch_bounds__(kMatchThreads) void k_match(const uint8_t *__restrict__ in, Layout L,
-                                                        uint32_t *__restrict__ m, uint64_t *__restrict__ chain,
-                                                        uint32_t *__restrict__ tile_exit,
-                                                        uint32_t *__restrict__ tile_flags) {
+constexpr uint32_t kWinPos = kHalo + 1 + kTile;      // 6144 window positions per tile
+constexpr uint32_t kMT = kMatchThreads;              // 512
+constexpr uint32_t kSeg = kTile / kMT;               // 8 positions per lane in the parse
+constexpr uint32_t kQPL = kTile / kMT;               // 8 queries per lane
+constexpr uint32_t kIlp = 4;                         // interleaved chain walks per lane
+constexpr uint32_t kWaves = kMT / 64;
+
+__device__ inline uint32_t key_mix(uint32_t key) { return (key * 0x9E3779B1u) & 0xFFFFFFu; }  // bijective mod 2^24
+
+struct Walk {
+    uint32_t c, x, xlo, cap, tag, best, bestx, steps, q1, q2;
+    bool unk;
+};
+
+__global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
+                                              uint64_t *__restrict__ chain, uint64_t *__restrict__ chain_pfx,
+                                              uint32_t *__restrict__ tinfo, uint32_t dbg) {
     __shared__ uint32_t sdw[kTileBytes / 4 + 4];           // byte image of the window
-    __shared__ uint32_t head[1u << kHashBits];             // bucket -> newest local index + 1
-    __shared__ uint16_t nxt[kHalo + 1 + kTile];            // older entry of the same bucket (+1)
-    __shared__ uint16_t step[kTile];                       // L+1 per tile position, 0 = unknown
-    __shared__ uint32_t Gs[kMatchThreads + 1];             // sub-segment entry points
-    __shared__ uint32_t Xs[kMatchThreads];                 // speculative sub-segment exits
-    __shared__ uint32_t Vs[kMatchThreads];                 // speculative visit masks
+    __shared__ uint32_t head[1u << kHashBits];             // bucket -> newest local index + 1;
+                                                           // after the queries: step[] + parse scratch
+    __shared__ uint32_t node[kWinPos];                     // (tag << 13) | (older index + 1)
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_chg[2];
+    __shared__ uint32_t s_red[3 * kWaves];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
@@ -60,97 +74,128 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(const uint8_t *__restri
     if ((((uintptr_t)src) & 3) == 0) {
         const uint32_t *src4 = (const uint32_t *)src;
         const uint32_t nfull = nload >> 2;
-        for (uint32_t x = tid; x < kTileBytes / 4 + 4; x += kMatchThreads) {
+        for (uint32_t x = tid; x < kTileBytes / 4 + 4; x += kMT) {
             uint32_t v = 0;
             if (x < nfull) v = src4[x];
-            else if (x == nfull) {
+            else if (x == nfull)
                 for (uint32_t q = 0; q < (nload & 3); q++) v |= (uint32_t)src[4 * x + q] << (8 * q);
-            }
             sdw[x] = v;
         }
     } else {
-        for (uint32_t x = tid; x < kTileBytes / 4 + 4; x += kMatchThreads) {
+        for (uint32_t x = tid; x < kTileBytes / 4 + 4; x += kMT) {
             uint32_t v = 0;
             for (uint32_t q = 0; q < 4; q++)
                 if (4 * x + q < nload) v |= (uint32_t)src[4 * x + q] << (8 * q);
             sdw[x] = v;
         }
     }
-    for (uint32_t x = tid; x < (1u << kHashBits); x += kMatchThreads) head[x] = 0;
+    for (uint32_t x = tid; x < (1u << kHashBits); x += kMT) head[x] = 0;
     if (tid == 0) { s_unknown = 0; s_chg[0] = 0; s_chg[1] = 0; }
     __syncthreads();
 
-    // ---- 2/3. insert + query in passes of 256 positions ----
+    // ---- 2. insert all window positions ----
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
-    for (uint32_t base = 0; base < npos; base += kMatchThreads) {
-        const uint32_t x = base + tid;
-        const uint32_t j = w0 + x;
-        if (x < npos && j + 3 <= blen) {
-            const uint32_t h = hash3(lds_key3(sdw, x));
-            const uint32_t old = atomicExch(&head[h], x + 1);
-            nxt[x] = (uint16_t)old;
-        }
-        __syncthreads();
-        if (x >= q0 && x < npos) {
-            const uint32_t i = j;
-            uint32_t res = 0, st = 1;
-            if (i != 0 && blen - i >= 4) {
-                if (s_unknown > kDenseUnknowns) {
-                    res = kUnknown; st = 0;   // dense tile: leave the rest to the stitch kernel
-                } else {
-                    const uint32_t cap = min(kMaxL, blen - i) - 1;
-                    const uint32_t key = lds_key3(sdw, x);
-                    const uint32_t xlo = (i > kWin ? i - kWin : 0) - w0;
-                    uint32_t best = kMinL - 1, bestx = 0xFFFFFFFFu, steps = 0;
-                    bool unk = false;
-                    for (uint32_t c = head[hash3(key)]; c != 0;) {
-                        const uint32_t xe = c - 1;
-                        if ((xe | (kMatchThreads - 1)) < xlo) break;  // whole pass below the window
-                        if (xe < x && xe >= xlo) {
-                            if (++steps > kMaxChainSteps) { unk = true; break; }
-                            if (lds_key3(sdw, xe) == key) {
-                                bool cand;
-                                if (best < kMinL) cand = true;
-                                else if (xe < bestx)   // may tie: needs L >= best
-                                    cand = lds_ld1(sdw, xe + best - 1) == lds_ld1(sdw, x + best - 1);
-                                else                   // must beat: needs L > best
-                                    cand = best < cap && lds_ld1(sdw, xe + best) == lds_ld1(sdw, x + best);
-                                if (cand) {
-                                    const uint32_t Lc = lds_match_len(sdw, xe, x, kMinL, cap);
-                                    if (Lc > best || (Lc == best && xe < bestx)) { best = Lc; bestx = xe; }
-                                }
-                            }
-                        }
-                        c = nxt[xe];
-                    }
-                    if (unk) { res = kUnknown; st = 0; atomicAdd(&s_unknown, 1u); }
-                    else if (best >= kMinL) { res = m_pack(best, x - bestx); st = best + 1; }
+    const uint32_t ins_end = min(npos, blen >= 3 ? blen - 2 - w0 : 0);  // j + 3 <= blen
+    for (uint32_t x = tid; x < ins_end; x += kMT) {
+        const uint32_t h = key_mix(lds_key3(sdw, x));
+        const uint32_t old = atomicExch(&head[h >> 12], x + 1);
+        node[x] = ((h & 0xFFFu) << 13) | old;
+    }
+    __syncthreads();
+
+    // ---- 3. queries: position i = w0 + q0 + tid + kMT*r, kIlp walks at a time ----
+    uint32_t st_reg[kQPL];
+#pragma unroll
+    for (uint32_t g = 0; g < kQPL; g += kIlp) {
+        Walk W[kIlp];
+#pragma unroll
+        for (uint32_t u = 0; u < kIlp; u++) {
+            Walk &w = W[u];
+            w.x = q0 + tid + kMT * (g + u);
+            w.c = 0; w.best = kMinL - 1; w.bestx = 0xFFFFFFFFu; w.steps = 0; w.unk = false;
+            w.cap = 0; w.xlo = 0; w.tag = 0; w.q1 = 0; w.q2 = 0;
+            if (w.x < npos) {
+                const uint32_t i = w0 + w.x;
+                if (i != 0 && blen - i >= 4 && !(dbg & 1u)) {
+                    w.cap = min(kMaxL, blen - i) - 1;
+                    const uint32_t h = key_mix(lds_key3(sdw, w.x));
+                    w.tag = h & 0xFFFu;
+                    w.xlo = (i > kWin ? i - kWin : 0) - w0;
+                    w.q1 = lds_ld4(sdw, w.x + 3);
+                    w.q2 = lds_ld4(sdw, w.x + 7);
+                    w.c = head[h >> 12];
                 }
             }
-            m[bstart + i] = res;
-            step[i - t0] = (uint16_t)st;
         }
-        __syncthreads();
+        for (;;) {
+            bool any = false;
+#pragma unroll
+            for (uint32_t u = 0; u < kIlp; u++) any |= W[u].c != 0;
+            if (!any) break;
+#pragma unroll
+            for (uint32_t u = 0; u < kIlp; u++) {
+                Walk &w = W[u];
+                if (w.c == 0) continue;
+                const uint32_t xe = w.c - 1;
+                const uint32_t nd = node[xe];
+                w.c = nd & 0x1FFFu;
+                if (++w.steps > kMaxChainSteps) { w.unk = true; w.c = 0; continue; }
+                if ((nd >> 13) != w.tag || xe >= w.x || xe < w.xlo) continue;
+                // common prefix with the query: bytes 0..2 equal by the key
+                uint32_t Lc;
+                const uint32_t a = lds_ld4(sdw, xe + 3) ^ w.q1;
+                if (a) {
+                    Lc = 3 + (__builtin_ctz(a) >> 3);
+                } else {
+                    const uint32_t bb = lds_ld4(sdw, xe + 7) ^ w.q2;
+                    if (bb) Lc = 7 + (__builtin_ctz(bb) >> 3);
+                    else Lc = (w.cap > 11 && !(dbg & 2u)) ? lds_match_len(sdw, xe, w.x, 11, w.cap) : 11;
+                }
+                Lc = min(Lc, w.cap);
+                if (Lc > w.best || (Lc == w.best && xe < w.bestx)) { w.best = Lc; w.bestx = xe; }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kIlp; u++) {
+            Walk &w = W[u];
+            uint32_t st = 1;
+            if (w.x < npos) {
+                uint32_t res = 0;
+                if (w.unk) { res = kUnknown; st = 0; s_unknown = 1; }
+                else if (w.best >= kMinL) { res = m_pack(w.best, w.x - w.bestx); st = w.best + 1; }
+                m[bstart + w0 + w.x] = res;
+            }
+            st_reg[g + u] = st;
+        }
+    }
+    __syncthreads();   // head[] is dead from here on
+
+    uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
+    uint32_t *ti = tinfo + 8ull * blockIdx.x;
+    const uint32_t nwords = (t1 - t0 + 63) / 64;
+    if (s_unknown != 0) {
+        for (uint32_t w = tid; w < nwords; w += kMT) cw[w] = 0;
+        if (tid == 0) { ti[0] = kTileLazy; ti[1] = 0; ti[2] = ti[3] = ti[4] = 0; }
+        return;
     }
 
     // ---- 4. tile-local greedy parse ----
-    uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
-    const uint32_t nwords = (t1 - t0 + 63) / 64;
-    if (s_unknown != 0) {
-        for (uint32_t w = tid; w < nwords; w += kMatchThreads) cw[w] = 0;
-        if (tid == 0) { tile_flags[blockIdx.x] = kTileLazy; tile_exit[blockIdx.x] = 0; }
-        return;
-    }
-    const uint32_t s = t0 + tid * kSubSeg;
-    const uint32_t se = min(s + kSubSeg, t1);
+    uint16_t *step = (uint16_t *)head;                 // 8 KB
+    uint32_t *Gs = head + kTile / 2;                   // kMT + 1 entries
+    uint32_t *Xs = Gs + kMT + 1;
+    uint32_t *Vs = Xs + kMT;
+#pragma unroll
+    for (uint32_t r = 0; r < kQPL; r++) step[tid + kMT * r] = (uint16_t)st_reg[r];
+    __syncthreads();
+    const uint32_t s = t0 + tid * kSeg;
+    const uint32_t se = min(s + kSeg, t1);
     uint32_t V = 0, X = s;
     if (s < t1) {
         uint32_t t = s;
         while (t < se) { V |= 1u << (t - s); t += step[t - t0]; }
         X = t;
     }
-    Vs[tid] = V;
     Xs[tid] = X;
     Gs[tid + 1] = X;
     if (tid == 0) Gs[0] = t0;
@@ -176,24 +221,58 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(const uint8_t *__restri
         __syncthreads();
         if (!s_chg[r & 1]) break;
     }
+    // counts of this lane's chain positions, prefix over lanes
+    uint32_t cnt[3] = {(uint32_t)__builtin_popcount(T), 0, 0};
+    for (uint32_t bits = T; bits; bits &= bits - 1) {
+        const uint32_t Lm = step[s - t0 + __builtin_ctz(bits)] - 1u;
+        if (Lm) { cnt[1]++; cnt[2] += (Lm >> 2) + 3; }
+    }
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    uint32_t inc[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) inc[q] = wave_incl_scan(cnt[q]);
+    if (lane == 63)
+        for (int q = 0; q < 3; q++) s_red[q * kWaves + wv] = inc[q];
     Vs[tid] = T;
     __syncthreads();
-    for (uint32_t w = tid; w < nwords; w += kMatchThreads) {
-        const uint64_t word = (uint64_t)Vs[4 * w] | ((uint64_t)Vs[4 * w + 1] << 16) |
-                              ((uint64_t)Vs[4 * w + 2] << 32) | ((uint64_t)Vs[4 * w + 3] << 48);
+    uint32_t pre[3], tot[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        uint32_t p = 0, a = 0;
+        for (uint32_t w = 0; w < kWaves; w++) {
+            const uint32_t v = s_red[q * kWaves + w];
+            if (w < wv) p += v;
+            a += v;
+        }
+        pre[q] = p + inc[q] - cnt[q];
+        tot[q] = a;
+    }
+    constexpr uint32_t kLanesPerWord = 64 / kSeg;   // 8
+    if ((tid % kLanesPerWord) == 0 && tid / kLanesPerWord < nwords) {
+        const uint32_t w = tid / kLanesPerWord;
+        uint64_t word = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kLanesPerWord; q++) word |= (uint64_t)Vs[tid + q] << (kSeg * q);
         cw[w] = word;
+        chain_pfx[(uint64_t)blockIdx.x * (kTile / 64) + w] =
+            (uint64_t)pre[0] | ((uint64_t)pre[1] << 13) | ((uint64_t)pre[2] << 24);
     }
     if (tid == 0) {
-        const uint32_t nsub = (t1 - t0 + kSubSeg - 1) / kSubSeg;
-        tile_flags[blockIdx.x] = 0;
-        tile_exit[blockIdx.x] = Gs[nsub];
+        const uint32_t nsub = (t1 - t0 + kSeg - 1) / kSeg;
+        ti[0] = 0;
+        ti[1] = Gs[nsub];
+        ti[2] = tot[0];
+        ti[3] = tot[1];
+        ti[4] = tot[2];
     }
 }
 
-void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint32_t *tile_exit,
-                  uint32_t *tile_flags, hipStream_t st) {
+void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint64_t *chain_pfx,
+                  uint32_t *tinfo, hipStream_t st) {
+    // FCX_MATCH_DBG (experiments only, output invalid when set): bit0 skip searches, bit1 skip long extension
+    static const uint32_t dbg = getenv("FCX_MATCH_DBG") ? (uint32_t)atoi(getenv("FCX_MATCH_DBG")) : 0u;
     const uint32_t grid = L.nblocks * L.tpb;
-    hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMatchThreads), 0, st, in, L, m, chain, tile_exit, tile_flags);
+    hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, chain, chain_pfx, tinfo, dbg);
 }
 
 }  // namespace fcx

@@ -4,19 +4,22 @@
 // chain: cursor += l + 1.  k_match resolved it inside each tile under the
 // assumption that a token starts at the tile's first position.  Here:
 //
-//   k_stitch      one wave per block walks the tiles in order with the true entry
-//                 point.  Fast path: the entry lies on the tile's speculative chain,
-//                 so the rest of the tile is already right (clear the bits before
-//                 it, jump to the tile exit).  Slow path: walk the true chain through
-//                 the tile's m[] (staged in LDS) until it meets the speculative chain;
-//                 positions k_match left unknown (dense windows) are evaluated here
-//                 by the whole wave: 64 candidates per step, oldest first, pruned by
-//                 the byte at the current best length, early exit at the cap.
-//   k_tile_count  tokens / matches / golomb bits per tile.
-//   k_block_scan  per-block exclusive scans of those counts + stream lengths.
-//   k_emit        writes the four streams of the block payload (make_bitMap_table
-//                 2073-2113, the split at 2150-2161, combine_bits 1292-1313,
-//                 golomb_rice_encode 258-304), staging bit words in LDS.
+//   k_stitch  one wave per block walks the tiles in order with the true entry
+//             point.  Fast path: the entry lies on the tile's speculative chain, so
+//             the rest of the tile is already right (clear the bits before it, jump
+//             to the tile exit).  Slow path: walk the true chain through the tile's
+//             m[] (staged in LDS) until it meets the speculative chain; positions
+//             k_match left unknown (dense windows) are evaluated by the whole wave:
+//             64 candidates per step, oldest first, pruned by the byte at the
+//             current best length, early exit at the cap.  Per-tile token / match /
+//             golomb-bit counts come from k_match's prefix counts minus the
+//             speculative positions dropped before the entry, and are scanned here
+//             into per-tile offsets and the block totals.
+//   k_emit    writes the four streams of the block payload (make_bitMap_table
+//             2073-2113, the split at 2150-2161, combine_bits 1292-1313,
+//             golomb_rice_encode 258-304): bits are gathered per lane, merged in
+//             LDS and stored as whole words (edge words of a tile by atomicOr);
+//             chars are staged in LDS and stored as aligned dwords.
 #include "fcx_device.h"
 
 namespace fcx {
@@ -74,7 +77,7 @@ __device__ void load_window(uint32_t *dw, const uint8_t *d, uint32_t dbase, uint
     }
 }
 
-// set bit `setb` (if < 4096) and clear bits [lo, hi) of an LDS bitmap, lane-parallel
+// set bit `setb` (if != ~0) and clear bits [lo, hi) of an LDS bitmap, lane-parallel
 __device__ inline void bm_apply(uint64_t *bm, uint32_t setb, uint32_t lo, uint32_t hi) {
     const uint32_t lane = lane_id();
     uint32_t first = 0xFFFFFFFFu, last = 0;
@@ -95,9 +98,37 @@ __device__ inline void bm_apply(uint64_t *bm, uint32_t setb, uint32_t lo, uint32
     }
 }
 
+struct Cnt3 {
+    uint32_t tok, mat, gb;
+    __device__ void add(uint32_t L) {
+        tok++;
+        if (L) { mat++; gb += (L >> 2) + 3; }
+    }
+};
+
+// counts of the speculative chain positions in [t0, t0 + rel): k_match's prefix
+// for the word plus the set bits of the (original) word below rel.  Wave-wide.
+__device__ Cnt3 spec_prefix(const uint64_t *pfx, const uint32_t *mt, uint64_t orig_word, uint32_t rel) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = rel >> 6, r = rel & 63;
+    const uint64_t p = pfx[w];
+    Cnt3 c{(uint32_t)(p & 0x1FFFu), (uint32_t)((p >> 13) & 0x7FFu), (uint32_t)((p >> 24) & 0x1FFFu)};
+    const uint64_t below = r ? (orig_word & ((1ull << r) - 1)) : 0ull;
+    uint32_t mt_ = 0, gb = 0;
+    if ((below >> lane) & 1ull) {
+        const uint32_t L = m_len(mt[w * 64 + lane]);
+        if (L) { mt_ = 1; gb = (L >> 2) + 3; }
+    }
+    c.tok += (uint32_t)__popcll(below);
+    c.mat += wave_sum_u32(mt_);
+    c.gb += wave_sum_u32(gb);
+    return c;
+}
+
 __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
-                                               uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_exit,
-                                               const uint32_t *__restrict__ tile_flags, BlockInfo *__restrict__ binfo) {
+                                               uint64_t *__restrict__ chain, const uint64_t *__restrict__ chain_pfx,
+                                               const uint32_t *__restrict__ tinfo, uint32_t *__restrict__ tile_off,
+                                               BlockInfo *__restrict__ binfo) {
     __shared__ uint32_t mL[kTile];
     __shared__ uint64_t bmL[kTile / 64];
     __shared__ uint32_t dw[kLazyWindow / 4 + 4];
@@ -109,39 +140,62 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
     const uint8_t *d = in + bstart;
     const uint32_t ntiles = (blen + kTile - 1) / kTile;
     uint32_t e = 0, dbase = 0xFFFFFFFFu, nlazy = 0, lazy_tiles = 0;
+    Cnt3 run{0, 0, 0};
 
     for (uint32_t k = 0; k < ntiles; k++) {
         const uint32_t t0 = k * kTile, t1 = min(blen, t0 + kTile);
         const uint32_t tix = b * L.tpb + k;
-        const bool lazy = (tile_flags[tix] & kTileLazy) != 0;
+        const uint32_t *ti = tinfo + 8ull * tix;
+        const bool lazy = (ti[0] & kTileLazy) != 0;
         uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
+        const uint64_t *pfx = chain_pfx + (uint64_t)tix * (kTile / 64);
+        const uint32_t *mt = m + bstart + t0;
         const uint32_t nw = (t1 - t0 + 63) / 64;
+        if (lane < 3) tile_off[3 * tix + lane] = lane == 0 ? run.tok : lane == 1 ? run.mat : run.gb;
         if (e >= t1) {  // a match spans the whole tile
             for (uint32_t w = lane; w < nw; w += 64) cw[w] = 0;
             continue;
         }
+        const Cnt3 tot{ti[2], ti[3], ti[4]};
         if (!lazy) {
             const uint32_t rel = e - t0;
             const uint64_t word = cw[rel >> 6];
             if ((word >> (rel & 63)) & 1ull) {  // converged at the entry
-                const uint32_t full = rel >> 6;
-                for (uint32_t w = lane; w < full; w += 64) cw[w] = 0;
-                if (lane == 0 && (rel & 63)) cw[full] = word & (~0ull << (rel & 63));
-                e = tile_exit[tix];
+                if (rel) {
+                    const Cnt3 drop = spec_prefix(pfx, mt, word, rel);
+                    run.tok += tot.tok - drop.tok;
+                    run.mat += tot.mat - drop.mat;
+                    run.gb += tot.gb - drop.gb;
+                    const uint32_t full = rel >> 6;
+                    for (uint32_t w = lane; w < full; w += 64) cw[w] = 0;
+                    if (lane == 0 && (rel & 63)) cw[full] = word & (~0ull << (rel & 63));
+                } else {
+                    run.tok += tot.tok; run.mat += tot.mat; run.gb += tot.gb;
+                }
+                e = ti[1];
                 continue;
             }
         }
         // ---- slow path ----
         lazy_tiles += lazy ? 1 : 0;
-        for (uint32_t x = lane; x < t1 - t0; x += 64) mL[x] = m[bstart + t0 + x];
+        for (uint32_t x = lane; x < t1 - t0; x += 64) mL[x] = mt[x];
         for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
         __syncthreads();
         if (e > t0) bm_apply(bmL, 0xFFFFFFFFu, 0, e - t0);
         __syncthreads();
         uint32_t t = e, exitv;
+        Cnt3 walked{0, 0, 0};
         for (;;) {
             const uint32_t rel = t - t0;
-            if (!lazy && ((bmL[rel >> 6] >> (rel & 63)) & 1ull)) { exitv = tile_exit[tix]; break; }
+            if (!lazy && ((bmL[rel >> 6] >> (rel & 63)) & 1ull)) {
+                // converged: the speculative chain from here on is the true one
+                const Cnt3 drop = spec_prefix(pfx, mt, cw[rel >> 6], rel);
+                walked.tok += tot.tok - drop.tok;
+                walked.mat += tot.mat - drop.mat;
+                walked.gb += tot.gb - drop.gb;
+                exitv = ti[1];
+                break;
+            }
             uint32_t mm = mL[rel];
             if (mm == kUnknown) {
                 const uint32_t lo = t > kWin ? t - kWin : 0;
@@ -155,43 +209,37 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 nlazy++;
                 if (lane == 0) m[bstart + t] = mm;
             }
+            walked.add(m_len(mm));
             const uint32_t nt = t + m_len(mm) + 1;
             bm_apply(bmL, rel, rel + 1, min(nt, t1) - t0);
             __syncthreads();
             t = nt;
             if (t >= t1) { exitv = t; break; }
         }
+        __syncthreads();
         for (uint32_t w = lane; w < nw; w += 64) cw[w] = bmL[w];
         __syncthreads();
+        run.tok += walked.tok; run.mat += walked.mat; run.gb += walked.gb;
         e = exitv;
     }
     if (lane == 0) {
-        binfo[b].lazy_evals = nlazy;
-        binfo[b].lazy_tiles = lazy_tiles;
+        BlockInfo &bi = binfo[b];
+        bi.len = blen;
+        bi.ntok = run.tok;
+        bi.nmatch = run.mat;
+        bi.gbits = run.gb;
+        bi.slen[0] = (run.tok + 7) / 8;                 // flags bytes (2078-2079)
+        bi.slen[1] = run.tok;                           // chars
+        bi.slen[2] = (kPBits * run.mat) / 8 + 1;        // (11*pCnt)/8 + 1 (2192)
+        bi.slen[3] = 4 * ((run.gb + 31) / 32);          // golomb words as bytes
+        bi.lazy_evals = nlazy;
+        bi.lazy_tiles = lazy_tiles;
     }
 }
 
 // ---------------------------------------------------------------------------
-// per-thread slice of a tile: 16 positions = one quarter of a chain word
-struct Slice {
-    uint32_t s, bits;
-};
-__device__ inline Slice tile_slice(const uint64_t *chain, const Layout &L, uint32_t b, uint32_t k, uint32_t t0,
-                                   uint32_t t1, uint32_t tid) {
-    Slice sl;
-    sl.s = t0 + tid * 16;
-    sl.bits = 0;
-    if (sl.s < t1) {
-        const uint64_t w = chain[(uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2)];
-        sl.bits = (uint32_t)(w >> (16 * (tid & 3))) & 0xFFFFu;
-        const uint32_t valid = min(16u, t1 - sl.s);
-        if (valid < 16) sl.bits &= (1u << valid) - 1;
-    }
-    return sl;
-}
-
 // block-wide exclusive scan of 3 counters (256 threads); returns totals in tot
-__device__ inline void block_scan3(uint32_t v[3], uint32_t tot[3], uint32_t *sh /* >= 3*4 */) {
+__device__ inline void block_scan3(uint32_t v[3], uint32_t tot[3], uint32_t *sh /* >= 12 */) {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     uint32_t inc[3];
 #pragma unroll
@@ -213,83 +261,40 @@ __device__ inline void block_scan3(uint32_t v[3], uint32_t tot[3], uint32_t *sh 
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_tile_count(Layout L, const uint32_t *__restrict__ m,
-                                                    const uint64_t *__restrict__ chain, uint32_t *__restrict__ tile_cnt) {
-    __shared__ uint32_t sh[12];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
-    const uint64_t bstart = (uint64_t)b * L.B;
-    const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
-    const uint32_t t0 = k * kTile;
-    if (t0 >= blen) return;
-    const uint32_t t1 = min(blen, t0 + kTile);
-    const Slice sl = tile_slice(chain, L, b, k, t0, t1, tid);
-    uint32_t v[3] = {(uint32_t)__builtin_popcount(sl.bits), 0, 0};
-    for (uint32_t bits = sl.bits; bits; bits &= bits - 1) {
-        const uint32_t L_ = m_len(m[bstart + sl.s + __builtin_ctz(bits)]);
-        if (L_) { v[1]++; v[2] += (L_ >> 2) + 3; }
-    }
-    uint32_t tot[3];
-    block_scan3(v, tot, sh);
-    if (tid == 0) {
-        tile_cnt[3 * blockIdx.x + 0] = tot[0];
-        tile_cnt[3 * blockIdx.x + 1] = tot[1];
-        tile_cnt[3 * blockIdx.x + 2] = tot[2];
-    }
-}
-
-__global__ __launch_bounds__(256) void k_block_scan(Layout L, const uint32_t *__restrict__ tile_cnt,
-                                                    uint32_t *__restrict__ tile_off, BlockInfo *__restrict__ binfo) {
-    __shared__ uint32_t sh[12];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;
-    const uint64_t bstart = (uint64_t)b * L.B;
-    const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
-    const uint32_t ntiles = (blen + kTile - 1) / kTile;
-    uint32_t carry[3] = {0, 0, 0};
-    for (uint32_t k0 = 0; k0 < ntiles; k0 += 256) {
-        const uint32_t k = k0 + tid;
-        uint32_t v[3] = {0, 0, 0};
-        if (k < ntiles)
-            for (int q = 0; q < 3; q++) v[q] = tile_cnt[3 * (b * L.tpb + k) + q];
-        uint32_t tot[3];
-        block_scan3(v, tot, sh);
-        if (k < ntiles)
-            for (int q = 0; q < 3; q++) tile_off[3 * (b * L.tpb + k) + q] = carry[q] + v[q];
-        for (int q = 0; q < 3; q++) carry[q] += tot[q];
-    }
-    if (tid == 0) {
-        BlockInfo &bi = binfo[b];
-        bi.len = blen;
-        bi.ntok = carry[0];
-        bi.nmatch = carry[1];
-        bi.gbits = carry[2];
-        bi.slen[0] = (carry[0] + 7) / 8;                 // flags bytes (2078-2079)
-        bi.slen[1] = carry[0];                           // chars
-        bi.slen[2] = (kPBits * carry[1]) / 8 + 1;        // (11*pCnt)/8 + 1 (2192)
-        bi.slen[3] = 4 * ((carry[2] + 31) / 32);         // golomb words as bytes
-    }
-}
-
 // LDS staging capacities per tile (words)
 constexpr uint32_t kFlagW = kTile / 32 + 2;
-constexpr uint32_t kPW = (kPBits * (kTile / 4)) / 32 + 3;
+constexpr uint32_t kPW = (kPBits * (kTile / 4 + 1)) / 32 + 4;
 constexpr uint32_t kGW = 128;
+constexpr uint32_t kCharW = kTile / 4 + 2;
 
-__device__ inline void or_bits_lds(uint32_t *w, uint32_t wbase, uint64_t pos, uint32_t val, uint32_t nbits) {
-    // OR nbits (<= 32) of val at absolute bit pos into staged words (word index relative to wbase)
-    const uint32_t wi = (uint32_t)(pos >> 5) - wbase, sh = (uint32_t)(pos & 31);
-    atomicOr(&w[wi], val << sh);
-    if (sh + nbits > 32) atomicOr(&w[wi + 1], val >> (32 - sh));
+// OR the low n (<= 64) bits of v at absolute bit pos into staged words (index relative to wbase)
+__device__ inline void or_bits64(uint32_t *w, uint32_t wbase, uint64_t pos, uint64_t v, uint32_t n) {
+    if (n == 0) return;
+    uint32_t wi = (uint32_t)(pos >> 5) - wbase, sh = (uint32_t)(pos & 31);
+    atomicOr(&w[wi], (uint32_t)(v << sh));
+    uint32_t done = 32 - sh;
+    while (done < n) {
+        wi++;
+        atomicOr(&w[wi], (uint32_t)(v >> done));
+        done += 32;
+    }
+}
+
+// store staged words [0, nw) at global word index gw0: edge words OR'd, interior stored
+__device__ inline void flush_words(uint32_t *g, uint32_t gw0, const uint32_t *w, uint32_t nw, uint32_t tid) {
+    for (uint32_t x = tid; x < nw; x += 256) {
+        const uint32_t v = w[x];
+        if (x == 0 || x == nw - 1) { if (v) atomicOr(&g[gw0 + x], v); }
+        else g[gw0 + x] = v;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
-                                              const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_cnt,
-                                              const uint32_t *__restrict__ tile_off, uint8_t *__restrict__ s_flags,
-                                              uint8_t *__restrict__ s_chars, uint8_t *__restrict__ s_p,
-                                              uint8_t *__restrict__ s_golomb) {
+                                              const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
+                                              uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
+                                              uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb) {
     __shared__ uint32_t sh[12];
-    __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW];
+    __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW], lc[kCharW];
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
     const uint64_t bstart = (uint64_t)b * L.B;
@@ -297,79 +302,105 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     const uint32_t t0 = k * kTile;
     if (t0 >= blen) return;
     const uint32_t t1 = min(blen, t0 + kTile);
-    const Slice sl = tile_slice(chain, L, b, k, t0, t1, tid);
 
-    uint32_t v[3] = {(uint32_t)__builtin_popcount(sl.bits), 0, 0};
-    for (uint32_t bits = sl.bits; bits; bits &= bits - 1) {
-        const uint32_t L_ = m_len(m[bstart + sl.s + __builtin_ctz(bits)]);
-        if (L_) { v[1]++; v[2] += (L_ >> 2) + 3; }
+    // this lane's 16 positions: one quarter of a chain word
+    const uint32_t s = t0 + tid * 16;
+    uint32_t bits = 0;
+    if (s < t1) {
+        const uint64_t w = chain[(uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2)];
+        bits = (uint32_t)(w >> (16 * (tid & 3))) & 0xFFFFu;
+        const uint32_t valid = min(16u, t1 - s);
+        if (valid < 16) bits &= (1u << valid) - 1;
+    }
+    const uint32_t *mt = m + bstart + s;
+    uint32_t mm[16];
+    uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0};
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++) {
+        mm[q] = ((bits >> q) & 1u) ? mt[q] : 0u;
+        const uint32_t Lq = m_len(mm[q]);
+        if (((bits >> q) & 1u) && Lq) { v[1]++; v[2] += (Lq >> 2) + 3; }
     }
     uint32_t tot[3];
+    const uint32_t nm_lane = v[1];
     block_scan3(v, tot, sh);
     const uint32_t tix = blockIdx.x;
     const uint32_t tok0 = tile_off[3 * tix + 0], mi0 = tile_off[3 * tix + 1], g0 = tile_off[3 * tix + 2];
-    uint32_t tok = tok0 + v[0], mi = mi0 + v[1], goff = g0 + v[2];
+    const uint32_t tokA = tok0 + v[0], miA = mi0 + v[1];
+    uint32_t goff = g0 + v[2];
     const uint32_t fw0 = tok0 >> 5, pw0 = (uint32_t)(((uint64_t)kPBits * mi0) >> 5), gw0 = g0 >> 5;
-    const uint32_t nfw = tot[0] ? ((tok0 + tot[0] - 1) >> 5) - fw0 + 1 : 0;
-    const uint32_t npw = tot[1] ? (uint32_t)(((uint64_t)kPBits * (mi0 + tot[1]) - 1) >> 5) - pw0 + 1 : 0;
-    const uint32_t ngw = tot[2] ? ((g0 + tot[2] - 1) >> 5) - gw0 + 1 : 0;
+    const uint32_t cw0 = tok0 >> 2;   // chars staged on the global dword grid
     for (uint32_t w = tid; w < kFlagW; w += 256) lf[w] = 0;
     for (uint32_t w = tid; w < kPW; w += 256) lp[w] = 0;
     for (uint32_t w = tid; w < kGW; w += 256) lg[w] = 0;
     __syncthreads();
 
     const uint8_t *d = in + bstart;
-    uint8_t *chars = s_chars + (uint64_t)b * L.sstride[1];
-    for (uint32_t bits = sl.bits; bits; bits &= bits - 1) {
-        const uint32_t i = sl.s + __builtin_ctz(bits);
-        const uint32_t mm = m[bstart + i];
-        const uint32_t Lm = m_len(mm);
-        chars[tok] = d[i + Lm];
-        if (Lm == 0) {
-            atomicOr(&lf[(tok >> 5) - fw0], 1u << (tok & 31));
-        } else {
-            or_bits_lds(lp, pw0, (uint64_t)kPBits * mi, m_dist(mm), kPBits);
-            const uint32_t q = Lm >> 2, r = Lm & 3;
-            // q one-bits, a zero bit, then r (2 bits, LSB first)
-            uint32_t pos = goff, left = q;
-            while (left) {
-                const uint32_t sh_ = pos & 31, n = min(left, 32 - sh_);
-                const uint32_t msk = (n == 32 ? ~0u : ((1u << n) - 1)) << sh_;
-                atomicOr(&lg[(pos >> 5) - gw0], msk);
-                pos += n;
-                left -= n;
+    uint8_t *lcb = (uint8_t *)lc;
+    uint32_t fl = 0, nt_lane = 0;
+    uint64_t pacc = 0;
+    uint32_t np_lane = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++) {
+        if ((bits >> q) & 1u) {
+            const uint32_t Lm = m_len(mm[q]);
+            lcb[tokA + nt_lane - 4 * cw0] = d[s + q + Lm];
+            if (Lm == 0) {
+                fl |= 1u << nt_lane;
+            } else {
+                pacc |= (uint64_t)m_dist(mm[q]) << (kPBits * np_lane);
+                np_lane++;
+                // q one-bits, a zero bit, then r (2 bits, LSB first)
+                const uint32_t qq = Lm >> 2, r = Lm & 3;
+                uint32_t pos = goff, left = qq;
+                while (left) {
+                    const uint32_t sh_ = pos & 31, n = min(left, 32 - sh_);
+                    const uint32_t msk = (n == 32 ? ~0u : ((1u << n) - 1)) << sh_;
+                    atomicOr(&lg[(pos >> 5) - gw0], msk);
+                    pos += n;
+                    left -= n;
+                }
+                pos += 1;
+                if (r) or_bits64(lg, gw0, pos, r, 2);
+                goff += qq + 3;
             }
-            pos += 1;
-            if (r) or_bits_lds(lg, gw0, pos, r, 2);
-            mi++;
-            goff += q + 3;
+            nt_lane++;
         }
-        tok++;
     }
+    or_bits64(lf, fw0, tokA, fl, nt_lane);
+    or_bits64(lp, pw0, (uint64_t)kPBits * miA, pacc, kPBits * nm_lane);
     __syncthreads();
-    uint32_t *fw = (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]);
-    uint32_t *pw = (uint32_t *)(s_p + (uint64_t)b * L.sstride[2]);
-    uint32_t *gw = (uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]);
-    for (uint32_t w = tid; w < nfw; w += 256) if (lf[w]) atomicOr(&fw[fw0 + w], lf[w]);
-    for (uint32_t w = tid; w < npw; w += 256) if (lp[w]) atomicOr(&pw[pw0 + w], lp[w]);
-    for (uint32_t w = tid; w < ngw; w += 256) if (lg[w]) atomicOr(&gw[gw0 + w], lg[w]);
+
+    // chars: aligned dwords inside the tile's range, bytes at its two edges
+    uint8_t *chars = s_chars + (uint64_t)b * L.sstride[1];
+    const uint32_t ce = tok0 + tot[0];   // end (exclusive) of this tile's chars
+    if (tot[0]) {
+        const uint32_t a = (tok0 + 3) & ~3u, z = ce & ~3u;   // [a, z) whole dwords
+        if (a < z) {
+            uint32_t *c4 = (uint32_t *)chars;
+            for (uint32_t w = (a >> 2) + tid; w < (z >> 2); w += 256) c4[w] = lc[w - cw0];
+        }
+        const uint32_t head_end = min(a, ce);
+        if (tid < head_end - tok0) chars[tok0 + tid] = lcb[tok0 + tid - 4 * cw0];
+        if (z >= a && tid < ce - z) chars[z + tid] = lcb[z + tid - 4 * cw0];
+    }
+    const uint32_t nfw = tot[0] ? ((tok0 + tot[0] - 1) >> 5) - fw0 + 1 : 0;
+    const uint32_t npw = tot[1] ? (uint32_t)(((uint64_t)kPBits * (mi0 + tot[1]) - 1) >> 5) - pw0 + 1 : 0;
+    const uint32_t ngw = tot[2] ? ((g0 + tot[2] - 1) >> 5) - gw0 + 1 : 0;
+    flush_words((uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]), fw0, lf, nfw, tid);
+    flush_words((uint32_t *)(s_p + (uint64_t)b * L.sstride[2]), pw0, lp, npw, tid);
+    flush_words((uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]), gw0, lg, ngw, tid);
 }
 
-void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint32_t *tile_exit,
-                  uint32_t *tile_flags, uint32_t *tile_cnt, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags,
-                  uint8_t *s_chars, uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, int stage,
-                  hipEvent_t *ev) {
-    (void)stage; (void)ev;
+void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, const uint64_t *chain_pfx,
+                  const uint32_t *tinfo, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
+                  uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev) {
     const uint32_t ntiles = L.nblocks * L.tpb;
-    hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, chain, tile_exit, tile_flags, binfo);
+    hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, chain, chain_pfx, tinfo, tile_off, binfo);
     if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(256), 0, st, L, m, chain, tile_cnt);
+    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, chain, tile_off, s_flags, s_chars, s_p,
+                       s_golomb);
     if (ev) (void)hipEventRecord(ev[1], st);
-    hipLaunchKernelGGL(k_block_scan, dim3(L.nblocks), dim3(256), 0, st, L, tile_cnt, tile_off, binfo);
-    if (ev) (void)hipEventRecord(ev[2], st);
-    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, chain, tile_cnt, tile_off, s_flags, s_chars,
-                       s_p, s_golomb);
-    if (ev) (void)hipEventRecord(ev[3], st);
 }
 
 }  // namespace fcx
