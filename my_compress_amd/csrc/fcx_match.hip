@@ -8,18 +8,18 @@
 // positions of one block:
 //
 //   1. stage [t0-2048, t1+260) of the block in LDS (dword loads);
-//   2. insert every window position into a 4096-bucket table of 3-byte keys.  The
-//      key is split by a bijection of Z/2^24 into (12-bit bucket, 12-bit tag), so
-//      a chain node {tag, next} identifies the key exactly and a chain step is one
-//      LDS read;
-//   3. every tile position walks its bucket (order irrelevant: all entries are
-//      visited) and keeps the max-length / min-position candidate among those in
-//      its window.  The walk is latency-bound, so each lane runs four walks
-//      interleaved; a candidate's length is read off two dword compares against
-//      the query's preloaded bytes 3..10, and only a match reaching 11 bytes
-//      enters the byte-by-dword extension loop.  A position seeing more than
-//      kMaxChainSteps entries is left "unknown" for the stitch kernel's
-//      wave-parallel evaluation (runs / zeros: long matches, few tokens);
+//   2. counting-sort every window position by the bucket of its 3-byte key: the
+//      key is split by a bijection of Z/2^24 into (12-bit bucket, 12-bit tag), an
+//      entry {tag, position} identifies the key exactly, and a bucket is one
+//      contiguous LDS range (count by LDS atomics, block scan, scatter);
+//   3. every tile position scans its bucket range (independent LDS loads, no
+//      pointer chase; four queries interleaved per lane) and keeps the
+//      max-length / min-position candidate among entries in its window.  A
+//      candidate's length is read off two dword compares against the query's
+//      preloaded bytes 3..10; only a match reaching 11 bytes enters the extension
+//      loop.  A bucket with more than kMaxChainSteps entries makes the position
+//      "unknown" at once, for the stitch kernel's wave-parallel evaluation
+//      (runs / zeros: long matches, few tokens);
 //   4. greedy parse of the tile assuming a token starts at t0: each lane walks
 //      its 8 positions, lanes agree on sub-segment entries by a Jacobi fixed
 //      point (entry_{k+1} = exit of sub-segment k walked from entry_k) that
@@ -41,7 +41,7 @@ constexpr uint32_t kWaves = kMT / 64;
 
 __device__ inline uint32_t key_mix(uint32_t key) { return (key * 0x9E3779B1u) & 0xFFFFFFu; }  // bijective mod 2^24
 
-struct Walk {
+struct Walk {   // one query: bucket range [c, c + steps), window [xlo, x), cap, key tag, bytes 3..10
     uint32_t c, x, xlo, cap, tag, best, bestx, steps, q1, q2;
     bool unk;
 };
@@ -50,12 +50,12 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
                                               uint64_t *__restrict__ chain, uint64_t *__restrict__ chain_pfx,
                                               uint32_t *__restrict__ tinfo, uint32_t dbg) {
     __shared__ uint32_t sdw[kTileBytes / 4 + 4];           // byte image of the window
-    __shared__ uint32_t head[1u << kHashBits];             // bucket -> newest local index + 1;
+    __shared__ uint32_t head[(1u << kHashBits) + 4];       // bucket -> count, then start of its range;
                                                            // after the queries: step[] + parse scratch
-    __shared__ uint32_t node[kWinPos];                     // (tag << 13) | (older index + 1)
+    __shared__ uint32_t node[kWinPos];                     // entries sorted by bucket: (tag << 13) | position
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_chg[2];
-    __shared__ uint32_t s_red[3 * kWaves];
+    __shared__ uint32_t s_red[3 * kWaves];   // cross-wave scan partials
 
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
@@ -89,26 +89,54 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
             sdw[x] = v;
         }
     }
-    for (uint32_t x = tid; x < (1u << kHashBits); x += kMT) head[x] = 0;
+    for (uint32_t x = tid; x < (1u << kHashBits) + 4; x += kMT) head[x] = 0;
     if (tid == 0) { s_unknown = 0; s_chg[0] = 0; s_chg[1] = 0; }
     __syncthreads();
 
-    // ---- 2. insert all window positions ----
+    // ---- 2. counting sort of the window positions by bucket ----
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
     const uint32_t ins_end = min(npos, blen >= 3 ? blen - 2 - w0 : 0);  // j + 3 <= blen
-    for (uint32_t x = tid; x < ins_end; x += kMT) {
-        const uint32_t h = key_mix(lds_key3(sdw, x));
-        const uint32_t old = atomicExch(&head[h >> 12], x + 1);
-        node[x] = ((h & 0xFFFu) << 13) | old;
+    constexpr uint32_t kIns = (kWinPos + kMT - 1) / kMT;               // 12 per lane
+    uint32_t ins_h[kIns], ins_r[kIns];
+#pragma unroll
+    for (uint32_t r = 0; r < kIns; r++) {
+        const uint32_t x = tid + kMT * r;
+        ins_h[r] = 0xFFFFFFFFu;
+        if (x < ins_end) {
+            ins_h[r] = key_mix(lds_key3(sdw, x));
+            ins_r[r] = atomicAdd(&head[ins_h[r] >> 12], 1u);
+        }
     }
     __syncthreads();
+    {   // exclusive scan of the 4096 bucket counts: 8 consecutive buckets per lane
+        constexpr uint32_t kPer = (1u << kHashBits) / kMT;
+        uint32_t cnt[kPer], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++) { cnt[q] = head[tid * kPer + q]; sum += cnt[q]; }
+        const uint32_t inc = wave_incl_scan(sum);
+        const uint32_t lane = tid & 63, wv = tid >> 6;
+        if (lane == 63) s_red[wv] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum;
+        for (uint32_t w = 0; w < wv; w++) run += s_red[w];
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++) { head[tid * kPer + q] = run; run += cnt[q]; }
+        if (tid == kMT - 1) head[1u << kHashBits] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kIns; r++)
+        if (ins_h[r] != 0xFFFFFFFFu)
+            node[head[ins_h[r] >> 12] + ins_r[r]] = ((ins_h[r] & 0xFFFu) << 13) | (tid + kMT * r);
+    __syncthreads();
 
-    // ---- 3. queries: position i = w0 + q0 + tid + kMT*r, kIlp walks at a time ----
+    // ---- 3. queries: position i = w0 + q0 + tid + kMT*r, kIlp at a time ----
     uint32_t st_reg[kQPL];
 #pragma unroll
     for (uint32_t g = 0; g < kQPL; g += kIlp) {
         Walk W[kIlp];
+        uint32_t nmax = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kIlp; u++) {
             Walk &w = W[u];
@@ -124,23 +152,20 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
                     w.xlo = (i > kWin ? i - kWin : 0) - w0;
                     w.q1 = lds_ld4(sdw, w.x + 3);
                     w.q2 = lds_ld4(sdw, w.x + 7);
-                    w.c = head[h >> 12];
+                    w.c = head[h >> 12];                       // range start
+                    w.steps = head[(h >> 12) + 1] - w.c;      // range length
+                    if (w.steps > kMaxChainSteps) { w.unk = true; w.steps = 0; }
+                    nmax = max(nmax, w.steps);
                 }
             }
         }
-        for (;;) {
-            bool any = false;
-#pragma unroll
-            for (uint32_t u = 0; u < kIlp; u++) any |= W[u].c != 0;
-            if (!any) break;
+        for (uint32_t j = 0; j < nmax; j++) {
 #pragma unroll
             for (uint32_t u = 0; u < kIlp; u++) {
                 Walk &w = W[u];
-                if (w.c == 0) continue;
-                const uint32_t xe = w.c - 1;
-                const uint32_t nd = node[xe];
-                w.c = nd & 0x1FFFu;
-                if (++w.steps > kMaxChainSteps) { w.unk = true; w.c = 0; continue; }
+                if (j >= w.steps) continue;
+                const uint32_t nd = node[w.c + j];
+                const uint32_t xe = nd & 0x1FFFu;
                 if ((nd >> 13) != w.tag || xe >= w.x || xe < w.xlo) continue;
                 // common prefix with the query: bytes 0..2 equal by the key
                 uint32_t Lc;
