@@ -13,10 +13,11 @@
 #include "fcx_device.h"
 
 namespace fcx {
-void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint64_t *chain_pfx,
-                  uint32_t *tinfo, hipStream_t st);
-void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, const uint64_t *chain_pfx,
-                  const uint32_t *tinfo, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
+void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                  uint64_t *chain_pfx, uint32_t *tinfo, hipStream_t st);
+void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
+                  const uint64_t *chain_pfx,
+                  const uint32_t *tinfo, uint64_t *fp, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
                   uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev);
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
                     uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_bits,
@@ -80,9 +81,11 @@ struct fcx_ctx {
     // scratch (device)
     uint32_t *m = nullptr;
     uint64_t *chain = nullptr;
+    uint64_t *mbits = nullptr;         // per position: m[] stored (match or unknown)
     uint64_t *chain_pfx = nullptr;     // per 64 positions: speculative prefix counts (k_match)
     uint32_t *tinfo = nullptr;         // per tile: flags, exit, token/match/golomb-bit totals
     uint32_t *tile_off = nullptr;      // per tile: token/match/golomb-bit offsets (k_stitch)
+    uint64_t *fp = nullptr;            // per tile: fast-path record (k_resolve)
     BlockInfo *binfo = nullptr;
     uint8_t *s[kStreams] = {nullptr, nullptr, nullptr, nullptr};
     uint32_t *hist = nullptr, *ctab = nullptr, *chunk_bits = nullptr;
@@ -105,12 +108,12 @@ struct fcx_ctx {
 
 namespace {
 void free_scratch(fcx_ctx *c) {
-    void *ptrs[] = {c->m,    c->chain, c->chain_pfx, c->tinfo,      c->tile_off, c->binfo,
+    void *ptrs[] = {c->m,    c->mbits, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->fp, c->binfo,
                     c->s[0], c->s[1],  c->s[2],      c->s[3],       c->hist,     c->ctab,     c->chunk_bits,
                     c->ltab, c->hhdr,  c->blk_off};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    c->m = nullptr; c->chain = c->chain_pfx = nullptr; c->tinfo = c->tile_off = nullptr;
+    c->m = nullptr; c->mbits = c->chain = c->chain_pfx = c->fp = nullptr; c->tinfo = c->tile_off = nullptr;
     c->binfo = nullptr;
     for (auto &p : c->s) p = nullptr;
     c->hist = c->ctab = c->chunk_bits = nullptr;
@@ -135,9 +138,11 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     int r;
     if ((r = dalloc(&c->m, 4ull * nb * c->B, "m"))) return r;
     if ((r = dalloc(&c->chain, 8ull * nb * L.wpb, "chain"))) return r;
+    if ((r = dalloc(&c->mbits, 8ull * nb * L.wpb, "mbits"))) return r;
     if ((r = dalloc(&c->chain_pfx, 8ull * (kTile / 64) * nt, "chain_pfx"))) return r;
     if ((r = dalloc(&c->tinfo, 32 * nt, "tinfo"))) return r;
     if ((r = dalloc(&c->tile_off, 12 * nt, "tile_off"))) return r;
+    if ((r = dalloc(&c->fp, 64 * nt, "fp"))) return r;
     if ((r = dalloc(&c->binfo, sizeof(BlockInfo) * nb, "binfo"))) return r;
     for (uint32_t s = 0; s < kStreams; s++)
         if ((r = dalloc(&c->s[s], (uint64_t)L.sstride[s] * nb + 64, "stream"))) return r;
@@ -287,9 +292,9 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     HIP_TRY(hipMemsetAsync(c->s[3], 0, (uint64_t)L.sstride[3] * L.nblocks, st));
     HIP_TRY(hipMemsetAsync(c->hist, 0, 4ull * 256 * kStreams * L.nblocks, st));
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
-    launch_match(d_in, L, c->m, c->chain, c->chain_pfx, c->tinfo, st);
+    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, st);
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
-    launch_parse(d_in, L, c->m, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->binfo, c->s[0], c->s[1], c->s[2],
+    launch_parse(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->fp, c->tile_off, c->binfo, c->s[0], c->s[1], c->s[2],
                  c->s[3], st, ev ? ev + 3 : nullptr);
     launch_entropy(L, c->binfo, c->s[0], c->s[1], c->s[2], c->s[3], c->hist, c->ctab, c->ltab, c->hhdr,
                    c->chunk_bits, c->blk_off, total, d_out, cap, err, st, ev ? ev + 5 : nullptr);

@@ -14,7 +14,9 @@
 //      contiguous LDS range (count by LDS atomics, block scan, scatter);
 //   3. every tile position scans its bucket range (independent LDS loads, no
 //      pointer chase; four queries interleaved per lane) and keeps the
-//      max-length / min-position candidate among entries in its window.  A
+//      max-length / min-position candidate among entries in its window (stored
+//      to m[] only where a match or "unknown" results, flagged per position in
+//      the mbits bitmap by one ballot per wave: random data writes almost no m).  A
 //      candidate's length is read off two dword compares against the query's
 //      preloaded bytes 3..10; only a match reaching 11 bytes enters the extension
 //      loop.  A bucket with more than kMaxChainSteps entries makes the position
@@ -47,7 +49,8 @@ struct Walk {   // one query: bucket range [c, c + steps), window [xlo, x), cap,
 };
 
 __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
-                                              uint64_t *__restrict__ chain, uint64_t *__restrict__ chain_pfx,
+                                              uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
+                                              uint64_t *__restrict__ chain_pfx,
                                               uint32_t *__restrict__ tinfo, uint32_t dbg) {
     __shared__ uint32_t sdw[kTileBytes / 4 + 4];           // byte image of the window
     __shared__ uint32_t head[(1u << kHashBits) + 4];       // bucket -> count, then start of its range;
@@ -184,13 +187,16 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
 #pragma unroll
         for (uint32_t u = 0; u < kIlp; u++) {
             Walk &w = W[u];
-            uint32_t st = 1;
+            uint32_t st = 1, res = 0;
             if (w.x < npos) {
-                uint32_t res = 0;
                 if (w.unk) { res = kUnknown; st = 0; s_unknown = 1; }
                 else if (w.best >= kMinL) { res = m_pack(w.best, w.x - w.bestx); st = w.best + 1; }
-                m[bstart + w0 + w.x] = res;
+                if (res) m[bstart + w0 + w.x] = res;   // m is stored only where mbits says so
             }
+            // the wave's 64 lanes hold 64 consecutive positions = one mbits word
+            const uint64_t mb = __ballot(res != 0);
+            const uint32_t xw = q0 + (tid & ~63u) + kMT * (g + u);
+            if ((tid & 63) == 0 && xw < npos) mbits[(uint64_t)b * L.wpb + ((w0 + xw) >> 6)] = mb;
             st_reg[g + u] = st;
         }
     }
@@ -292,12 +298,12 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
     }
 }
 
-void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, uint64_t *chain_pfx,
+void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                   uint32_t *tinfo, hipStream_t st) {
     // FCX_MATCH_DBG (experiments only, output invalid when set): bit0 skip searches, bit1 skip long extension
     static const uint32_t dbg = getenv("FCX_MATCH_DBG") ? (uint32_t)atoi(getenv("FCX_MATCH_DBG")) : 0u;
     const uint32_t grid = L.nblocks * L.tpb;
-    hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, chain, chain_pfx, tinfo, dbg);
+    hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, dbg);
 }
 
 }  // namespace fcx

@@ -4,10 +4,13 @@
 // chain: cursor += l + 1.  k_match resolved it inside each tile under the
 // assumption that a token starts at the tile's first position.  Here:
 //
+//   k_resolve one wave per tile, all tiles in parallel: assuming the entry is the
+//             previous tile's speculative exit, walk the true chain until it meets
+//             this tile's speculative chain and record the corrected counts, exit
+//             and rewritten chain words.
 //   k_stitch  one wave per block walks the tiles in order with the true entry
-//             point.  Fast path: the entry lies on the tile's speculative chain, so
-//             the rest of the tile is already right (clear the bits before it, jump
-//             to the tile exit).  Slow path: walk the true chain through the tile's
+//             point.  Fast path: the entry is the one k_resolve assumed, so commit
+//             its record (counts, exit, <= 4 chain words).  Slow path: walk the true chain through the tile's
 //             m[] (staged in LDS) until it meets the speculative chain; positions
 //             k_match left unknown (dense windows) are evaluated by the whole wave:
 //             64 candidates per step, oldest first, pruned by the byte at the
@@ -108,14 +111,15 @@ struct Cnt3 {
 
 // counts of the speculative chain positions in [t0, t0 + rel): k_match's prefix
 // for the word plus the set bits of the (original) word below rel.  Wave-wide.
-__device__ Cnt3 spec_prefix(const uint64_t *pfx, const uint32_t *mt, uint64_t orig_word, uint32_t rel) {
+__device__ Cnt3 spec_prefix(const uint64_t *pfx, const uint32_t *mt, const uint64_t *mb, uint64_t orig_word,
+                            uint32_t rel) {
     const uint32_t lane = lane_id();
     const uint32_t w = rel >> 6, r = rel & 63;
     const uint64_t p = pfx[w];
     Cnt3 c{(uint32_t)(p & 0x1FFFu), (uint32_t)((p >> 13) & 0x7FFu), (uint32_t)((p >> 24) & 0x1FFFu)};
     const uint64_t below = r ? (orig_word & ((1ull << r) - 1)) : 0ull;
     uint32_t mt_ = 0, gb = 0;
-    if ((below >> lane) & 1ull) {
+    if ((below >> lane) & (mb[w] >> lane) & 1ull) {
         const uint32_t L = m_len(mt[w * 64 + lane]);
         if (L) { mt_ = 1; gb = (L >> 2) + 3; }
     }
@@ -125,12 +129,134 @@ __device__ Cnt3 spec_prefix(const uint64_t *pfx, const uint32_t *mt, uint64_t or
     return c;
 }
 
+// Fast-path resolution per tile, for all tiles in parallel ahead of the
+// sequential stitch.  Assume the true entry is the previous tile's speculative
+// exit (it is whenever the previous tile was resolved this way) and walk the
+// greedy chain from it until it meets this tile's speculative chain — usually
+// within a few tokens.  Recorded per tile (fp[8*tix]):
+//   [0] ok | rel << 1 (assumed entry - t0) | nmod << 16 (chain words rewritten)
+//   [1] tokens | matches << 32, [2] golomb bits (the tile's final counts)
+//   [3] exit (first chain position >= t1)
+//   [4..7] the rewritten chain words 0..3 (positions t0 .. t0+255)
+// ok = 0 when the walk needs > 256 positions, meets an unknown position, or a
+// neighbour is lazy: the stitch then walks the tile itself.
+constexpr uint32_t kResolveSpan = 256;
+
+__global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__restrict__ m,
+                                                const uint64_t *__restrict__ mbits,
+                                                const uint64_t *__restrict__ chain,
+                                                const uint64_t *__restrict__ chain_pfx,
+                                                const uint32_t *__restrict__ tinfo, uint64_t *__restrict__ fp) {
+    const uint32_t lane = threadIdx.x, tix = blockIdx.x;
+    const uint32_t b = tix / L.tpb, k = tix % L.tpb;
+    const uint64_t bstart = (uint64_t)b * L.B;
+    const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
+    const uint32_t t0 = k * kTile;
+    if (t0 >= blen) return;
+    const uint32_t t1 = min(blen, t0 + kTile);
+    uint64_t *out = fp + 8ull * tix;
+    const uint32_t *ti = tinfo + 8ull * tix;
+    bool ok = (ti[0] & kTileLazy) == 0;
+    uint32_t ea = t0;
+    if (ok && k > 0) {
+        const uint32_t *tp = tinfo + 8ull * (tix - 1);
+        ok = (tp[0] & kTileLazy) == 0;
+        ea = tp[1];
+    }
+    ok = ok && ea < t1 && ea - t0 < kResolveSpan;
+    if (!ok) {
+        if (lane == 0) out[0] = 0;
+        return;
+    }
+    const uint32_t rel0 = ea - t0;
+    const uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
+    const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
+    const uint32_t *mt = m + bstart + t0;
+    const uint32_t nw = min(4u, (t1 - t0 + 63) / 64);
+    // prefetch: chain + mbits words 0..3 (lanes 0..3), m of positions t0..t0+255 (4 per lane)
+    uint64_t wv = 0, mv = 0;
+    if (lane < nw) { wv = cw[lane]; mv = mb[lane]; }
+    uint32_t mreg[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t x = 64 * q + lane;
+        const uint64_t mbq = __shfl(mv, q, 64);
+        mreg[q] = (x < t1 - t0 && ((mbq >> lane) & 1ull)) ? mt[x] : 0u;
+    }
+    uint64_t orig[4], mbw[4], nwb[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) { orig[q] = __shfl(wv, q, 64); mbw[q] = __shfl(mv, q, 64); nwb[q] = 0; }
+    // walk from the assumed entry until it meets the speculative chain (uniform over the wave)
+    Cnt3 walked{0, 0, 0};
+    uint32_t rel = rel0, exitv = 0;
+    bool conv = false;
+    for (;;) {
+        if (rel >= t1 - t0) { exitv = t0 + rel; break; }
+        if (rel >= kResolveSpan) { ok = false; break; }
+        const uint32_t q = rel >> 6, r = rel & 63;
+        uint64_t o = orig[0], mbq = mbw[0];
+#pragma unroll
+        for (uint32_t u = 1; u < 4; u++) if (q == u) { o = orig[u]; mbq = mbw[u]; }
+        if ((o >> r) & 1ull) { conv = true; break; }
+        uint32_t mm = 0;
+        if ((mbq >> r) & 1ull) {
+            uint32_t v = mreg[0];
+#pragma unroll
+            for (uint32_t u = 1; u < 4; u++) if (q == u) v = mreg[u];
+            mm = __shfl(v, r, 64);
+        }
+        if (mm == kUnknown) { ok = false; break; }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) if (q == u) nwb[u] |= 1ull << r;
+        walked.add(m_len(mm));
+        rel += m_len(mm) + 1;
+    }
+    if (!ok) {
+        if (lane == 0) out[0] = 0;
+        return;
+    }
+    Cnt3 fin = walked;
+    uint32_t keep_from = rel;   // speculative bits at positions >= keep_from stay
+    if (conv) {
+        const Cnt3 drop = rel ? spec_prefix(chain_pfx + (uint64_t)tix * (kTile / 64), mt, mb, orig[rel >> 6], rel)
+                              : Cnt3{0, 0, 0};
+        fin.tok += ti[2] - drop.tok;
+        fin.mat += ti[3] - drop.mat;
+        fin.gb += ti[4] - drop.gb;
+        exitv = ti[1];
+    } else {
+        keep_from = t1 - t0;   // the walk covered the rest of the tile
+    }
+    // rewritten words: walked bits below keep_from, speculative bits from keep_from on
+    const uint32_t nmod = min(nw, (min(keep_from, kResolveSpan) + 63) / 64);
+    if (lane == 0) {
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t lo = 64 * u;
+            uint64_t keepmask;
+            if (keep_from <= lo) keepmask = ~0ull;
+            else if (keep_from >= lo + 64) keepmask = 0;
+            else keepmask = ~0ull << (keep_from - lo);
+            out[4 + u] = (orig[u] & keepmask) | nwb[u];
+        }
+        out[0] = 1ull | ((uint64_t)rel0 << 1) | ((uint64_t)nmod << 16);
+        out[1] = (uint64_t)fin.tok | ((uint64_t)fin.mat << 32);
+        out[2] = fin.gb;
+        out[3] = exitv;
+    }
+    (void)conv;
+}
+
 __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
-                                               uint64_t *__restrict__ chain, const uint64_t *__restrict__ chain_pfx,
-                                               const uint32_t *__restrict__ tinfo, uint32_t *__restrict__ tile_off,
-                                               BlockInfo *__restrict__ binfo) {
+                                               const uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain, const uint64_t *__restrict__ chain_pfx,
+                                               const uint32_t *__restrict__ tinfo, const uint64_t *__restrict__ fp,
+                                               uint32_t *__restrict__ tile_off, BlockInfo *__restrict__ binfo) {
     __shared__ uint32_t mL[kTile];
+    __shared__ uint32_t sti[64][6];          // per tile of the batch: flags, exit, totals, k_resolve verdict
+    __shared__ uint32_t sfp[64][4];          // k_resolve: final counts, exit
+    __shared__ uint64_t sfw[64][4];          // k_resolve: rewritten chain words
     __shared__ uint64_t bmL[kTile / 64];
+    __shared__ uint64_t mbL[kTile / 64];
     __shared__ uint32_t dw[kLazyWindow / 4 + 4];
 
     const uint32_t lane = threadIdx.x;
@@ -145,10 +271,30 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
     for (uint32_t k = 0; k < ntiles; k++) {
         const uint32_t t0 = k * kTile, t1 = min(blen, t0 + kTile);
         const uint32_t tix = b * L.tpb + k;
-        const uint32_t *ti = tinfo + 8ull * tix;
-        const bool lazy = (ti[0] & kTileLazy) != 0;
+        const uint32_t j = k & 63;
+        if (j == 0) {   // prefetch the next 64 tiles' info (independent loads, one tile per lane)
+            __syncthreads();
+            const uint32_t kk = k + lane;
+            if (kk < ntiles) {
+                const uint32_t *tq = tinfo + 8ull * (b * L.tpb + kk);
+                const uint64_t *fq = fp + 8ull * (b * L.tpb + kk);
+                sti[lane][0] = tq[0]; sti[lane][1] = tq[1]; sti[lane][2] = tq[2];
+                sti[lane][3] = tq[3]; sti[lane][4] = tq[4];
+                const uint64_t f0 = fq[0];
+                sti[lane][5] = (uint32_t)f0;
+                if (f0 & 1ull) {
+                    const uint64_t f1 = fq[1];
+                    sfp[lane][0] = (uint32_t)f1; sfp[lane][1] = (uint32_t)(f1 >> 32);
+                    sfp[lane][2] = (uint32_t)fq[2]; sfp[lane][3] = (uint32_t)fq[3];
+                    for (uint32_t u = 0; u < 4; u++) sfw[lane][u] = fq[4 + u];
+                }
+            }
+            __syncthreads();
+        }
+        const bool lazy = (sti[j][0] & kTileLazy) != 0;
         uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
         const uint64_t *pfx = chain_pfx + (uint64_t)tix * (kTile / 64);
+        const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
         const uint32_t *mt = m + bstart + t0;
         const uint32_t nw = (t1 - t0 + 63) / 64;
         if (lane < 3) tile_off[3 * tix + lane] = lane == 0 ? run.tok : lane == 1 ? run.mat : run.gb;
@@ -156,29 +302,23 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
             for (uint32_t w = lane; w < nw; w += 64) cw[w] = 0;
             continue;
         }
-        const Cnt3 tot{ti[2], ti[3], ti[4]};
-        if (!lazy) {
-            const uint32_t rel = e - t0;
-            const uint64_t word = cw[rel >> 6];
-            if ((word >> (rel & 63)) & 1ull) {  // converged at the entry
-                if (rel) {
-                    const Cnt3 drop = spec_prefix(pfx, mt, word, rel);
-                    run.tok += tot.tok - drop.tok;
-                    run.mat += tot.mat - drop.mat;
-                    run.gb += tot.gb - drop.gb;
-                    const uint32_t full = rel >> 6;
-                    for (uint32_t w = lane; w < full; w += 64) cw[w] = 0;
-                    if (lane == 0 && (rel & 63)) cw[full] = word & (~0ull << (rel & 63));
-                } else {
-                    run.tok += tot.tok; run.mat += tot.mat; run.gb += tot.gb;
-                }
-                e = ti[1];
-                continue;
-            }
+        const Cnt3 tot{sti[j][2], sti[j][3], sti[j][4]};
+        const uint32_t fpv = sti[j][5];
+        if ((fpv & 1u) && e - t0 == ((fpv >> 1) & 0x7FFFu)) {   // entry = the one k_resolve assumed
+            run.tok += sfp[j][0];
+            run.mat += sfp[j][1];
+            run.gb += sfp[j][2];
+            const uint32_t nmod = fpv >> 16;
+            if (lane < nmod) cw[lane] = sfw[j][lane];
+            e = sfp[j][3];
+            continue;
         }
         // ---- slow path ----
         lazy_tiles += lazy ? 1 : 0;
-        for (uint32_t x = lane; x < t1 - t0; x += 64) mL[x] = mt[x];
+        mbL[lane] = lane < nw ? mb[lane] : 0ull;   // one mbits word per lane (64 words per tile)
+        __syncthreads();
+        for (uint32_t x = lane; x < t1 - t0; x += 64)   // m only where the position's mbits bit is set
+            mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? mt[x] : 0u;
         for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
         __syncthreads();
         if (e > t0) bm_apply(bmL, 0xFFFFFFFFu, 0, e - t0);
@@ -189,11 +329,11 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
             const uint32_t rel = t - t0;
             if (!lazy && ((bmL[rel >> 6] >> (rel & 63)) & 1ull)) {
                 // converged: the speculative chain from here on is the true one
-                const Cnt3 drop = spec_prefix(pfx, mt, cw[rel >> 6], rel);
+                const Cnt3 drop = spec_prefix(pfx, mt, mb, cw[rel >> 6], rel);
                 walked.tok += tot.tok - drop.tok;
                 walked.mat += tot.mat - drop.mat;
                 walked.gb += tot.gb - drop.gb;
-                exitv = ti[1];
+                exitv = sti[j][1];
                 break;
             }
             uint32_t mm = mL[rel];
@@ -290,7 +430,7 @@ __device__ inline void flush_words(uint32_t *g, uint32_t gw0, const uint32_t *w,
 }
 
 __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
-                                              const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
+                                              const uint64_t *__restrict__ mbits, const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb) {
     __shared__ uint32_t sh[12];
@@ -305,19 +445,21 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
 
     // this lane's 16 positions: one quarter of a chain word
     const uint32_t s = t0 + tid * 16;
-    uint32_t bits = 0;
+    uint32_t bits = 0, mbs = 0;
     if (s < t1) {
-        const uint64_t w = chain[(uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2)];
-        bits = (uint32_t)(w >> (16 * (tid & 3))) & 0xFFFFu;
+        const uint64_t wi = (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2);
+        bits = (uint32_t)(chain[wi] >> (16 * (tid & 3))) & 0xFFFFu;
+        mbs = (uint32_t)(mbits[wi] >> (16 * (tid & 3))) & 0xFFFFu;
         const uint32_t valid = min(16u, t1 - s);
         if (valid < 16) bits &= (1u << valid) - 1;
     }
+    const uint32_t rd = bits & mbs;   // chain positions whose m is stored
     const uint32_t *mt = m + bstart + s;
     uint32_t mm[16];
     uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0};
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
-        mm[q] = ((bits >> q) & 1u) ? mt[q] : 0u;
+        mm[q] = ((rd >> q) & 1u) ? mt[q] : 0u;
         const uint32_t Lq = m_len(mm[q]);
         if (((bits >> q) & 1u) && Lq) { v[1]++; v[2] += (Lq >> 2) + 3; }
     }
@@ -392,14 +534,17 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     flush_words((uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]), gw0, lg, ngw, tid);
 }
 
-void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *chain, const uint64_t *chain_pfx,
-                  const uint32_t *tinfo, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
+void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
+                  const uint64_t *chain_pfx,
+                  const uint32_t *tinfo, uint64_t *fp, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
                   uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev) {
     const uint32_t ntiles = L.nblocks * L.tpb;
-    hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, chain, chain_pfx, tinfo, tile_off, binfo);
+    hipLaunchKernelGGL(k_resolve, dim3(ntiles), dim3(64), 0, st, L, m, mbits, chain, chain_pfx, tinfo, fp);
+    hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, tile_off,
+                       binfo);
     if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, chain, tile_off, s_flags, s_chars, s_p,
-                       s_golomb);
+    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, s_flags, s_chars,
+                       s_p, s_golomb);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 
