@@ -33,7 +33,8 @@ class FcxError(RuntimeError):
 
 
 def lib_path() -> str:
-    return os.path.join(PKG_DIR, "lib", "libfcx.so")
+    # FCX_LIB: alternative in-tree build for A/B experiments (tools/); default lib/libfcx.so
+    return os.environ.get("FCX_LIB") or os.path.join(PKG_DIR, "lib", "libfcx.so")
 
 
 def lib():

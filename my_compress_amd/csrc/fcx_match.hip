@@ -8,18 +8,19 @@
 // positions of one block:
 //
 //   1. stage [t0-2048, t1+260) of the block in LDS (dword loads);
-//   2. counting-sort every window position by the bucket of its 3-byte key: the
-//      key is split by a bijection of Z/2^24 into (12-bit bucket, 12-bit tag), an
-//      entry {tag, position} identifies the key exactly, and a bucket is one
-//      contiguous LDS range (count by LDS atomics, block scan, scatter);
+//   2. counting-sort every window position by the bucket of its 3-byte key (a
+//      bijection of Z/2^24 gives a 12-bit bucket; 16-bit entries keep the position
+//      and 3 more hash bits, the rare collisions are rejected by comparing key
+//      bytes); a bucket is one contiguous LDS range (16-bit counters by LDS
+//      atomics, block scan, scatter);
 //   3. every tile position scans its bucket range (independent LDS loads, no
 //      pointer chase; four queries interleaved per lane) and keeps the
 //      max-length / min-position candidate among entries in its window (stored
 //      to m[] only where a match or "unknown" results, flagged per position in
 //      the mbits bitmap by one ballot per wave: random data writes almost no m).  A
-//      candidate's length is read off two dword compares against the query's
-//      preloaded bytes 3..10; only a match reaching 11 bytes enters the extension
-//      loop.  A bucket with more than kMaxChainSteps entries makes the position
+//      candidate's key check and length come from three dword compares against
+//      the query's preloaded bytes 0..11; only a match reaching 12 bytes enters
+//      the extension loop.  A bucket with more than kMaxChainSteps entries makes the position
 //      "unknown" at once, for the stitch kernel's wave-parallel evaluation
 //      (runs / zeros: long matches, few tokens);
 //   4. greedy parse of the tile assuming a token starts at t0: each lane walks
@@ -40,22 +41,24 @@ constexpr uint32_t kSeg = kTile / kMT;               // 8 positions per lane in 
 constexpr uint32_t kQPL = kTile / kMT;               // 8 queries per lane
 constexpr uint32_t kIlp = 4;                         // interleaved chain walks per lane
 constexpr uint32_t kWaves = kMT / 64;
+constexpr uint32_t kHeadWords = (1u << kHashBits) / 2 + 4;                 // u16 counters + sentinel
+constexpr uint32_t kEntWords = kWinPos / 2;                                 // u16 entries
+constexpr uint32_t kRegionWords = kHeadWords + kEntWords > kTile / 2 + 3 * kMT + 1
+                                      ? kHeadWords + kEntWords : kTile / 2 + 3 * kMT + 1;
 
 __device__ inline uint32_t key_mix(uint32_t key) { return (key * 0x9E3779B1u) & 0xFFFFFFu; }  // bijective mod 2^24
 
-struct Walk {   // one query: bucket range [c, c + steps), window [xlo, x), cap, key tag, bytes 3..10
-    uint32_t c, x, xlo, cap, tag, best, bestx, steps, q1, q2;
-    bool unk;
-};
-
-__global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
+__global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
                                               uint32_t *__restrict__ tinfo, uint32_t dbg) {
     __shared__ uint32_t sdw[kTileBytes / 4 + 4];           // byte image of the window
-    __shared__ uint32_t head[(1u << kHashBits) + 4];       // bucket -> count, then start of its range;
-                                                           // after the queries: step[] + parse scratch
-    __shared__ uint32_t node[kWinPos];                     // entries sorted by bucket: (tag << 13) | position
+    // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
+    // search, [step (u16 x 4096) | parse scratch] after it
+    __shared__ uint32_t region[kRegionWords];
+    uint32_t *hw = region;                                  // packed u16 bucket counters, then starts
+    uint16_t *h16 = (uint16_t *)region;
+    uint16_t *ent = (uint16_t *)(region + kHeadWords);     // window entries, bucket-sorted
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_chg[2];
     __shared__ uint32_t s_red[3 * kWaves];   // cross-wave scan partials
@@ -92,31 +95,33 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
             sdw[x] = v;
         }
     }
-    for (uint32_t x = tid; x < (1u << kHashBits) + 4; x += kMT) head[x] = 0;
+    for (uint32_t x = tid; x < kHeadWords; x += kMT) hw[x] = 0;
     if (tid == 0) { s_unknown = 0; s_chg[0] = 0; s_chg[1] = 0; }
     __syncthreads();
 
     // ---- 2. counting sort of the window positions by bucket ----
+    // 16-bit counters, two per dword (a bucket never exceeds 6144 entries)
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
     const uint32_t ins_end = min(npos, blen >= 3 ? blen - 2 - w0 : 0);  // j + 3 <= blen
     constexpr uint32_t kIns = (kWinPos + kMT - 1) / kMT;               // 12 per lane
-    uint32_t ins_h[kIns], ins_r[kIns];
+    uint32_t ins_hr[kIns];                                             // bucket << 16 | rank
 #pragma unroll
     for (uint32_t r = 0; r < kIns; r++) {
         const uint32_t x = tid + kMT * r;
-        ins_h[r] = 0xFFFFFFFFu;
+        ins_hr[r] = 0xFFFFFFFFu;
         if (x < ins_end) {
-            ins_h[r] = key_mix(lds_key3(sdw, x));
-            ins_r[r] = atomicAdd(&head[ins_h[r] >> 12], 1u);
+            const uint32_t h = key_mix(lds_key3(sdw, x));
+            const uint32_t bk = h >> 12, sh = 16 * (bk & 1);
+            const uint32_t old = atomicAdd(&hw[bk >> 1], 1u << sh);
+            ins_hr[r] = (bk << 16) | ((old >> sh) & 0xFFFFu);
         }
     }
     __syncthreads();
-    {   // exclusive scan of the 4096 bucket counts: 8 consecutive buckets per lane
-        constexpr uint32_t kPer = (1u << kHashBits) / kMT;
-        uint32_t cnt[kPer], sum = 0;
+    {   // exclusive scan of the 4096 bucket counts: 8 consecutive buckets (4 dwords) per lane
+        uint32_t cw4[4], sum = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < kPer; q++) { cnt[q] = head[tid * kPer + q]; sum += cnt[q]; }
+        for (uint32_t q = 0; q < 4; q++) { cw4[q] = hw[tid * 4 + q]; sum += (cw4[q] & 0xFFFFu) + (cw4[q] >> 16); }
         const uint32_t inc = wave_incl_scan(sum);
         const uint32_t lane = tid & 63, wv = tid >> 6;
         if (lane == 63) s_red[wv] = inc;
@@ -124,83 +129,104 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
         uint32_t run = inc - sum;
         for (uint32_t w = 0; w < wv; w++) run += s_red[w];
 #pragma unroll
-        for (uint32_t q = 0; q < kPer; q++) { head[tid * kPer + q] = run; run += cnt[q]; }
-        if (tid == kMT - 1) head[1u << kHashBits] = run;
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t lo = run, hi = run + (cw4[q] & 0xFFFFu);
+            run = hi + (cw4[q] >> 16);
+            hw[tid * 4 + q] = lo | (hi << 16);
+        }
+        if (tid == kMT - 1) hw[(1u << kHashBits) / 2] = run;   // start[4096] = total
     }
     __syncthreads();
+    // scatter into bucket order: entry = position | 3 more hash bits << 13
 #pragma unroll
     for (uint32_t r = 0; r < kIns; r++)
-        if (ins_h[r] != 0xFFFFFFFFu)
-            node[head[ins_h[r] >> 12] + ins_r[r]] = ((ins_h[r] & 0xFFFu) << 13) | (tid + kMT * r);
+        if (ins_hr[r] != 0xFFFFFFFFu) {
+            const uint32_t x = tid + kMT * r;
+            const uint32_t bk = ins_hr[r] >> 16;
+            const uint32_t h = key_mix(lds_key3(sdw, x));
+            ent[h16[bk] + (ins_hr[r] & 0xFFFFu)] = (uint16_t)(((h & 7u) << 13) | x);
+        }
     __syncthreads();
 
     // ---- 3. queries: position i = w0 + q0 + tid + kMT*r, kIlp at a time ----
-    uint32_t st_reg[kQPL];
+    // per walk: range (start | len << 16), packed best = L << 13 | (8191 - position),
+    // query bytes 0..11, x | cap << 13 | tag3 << 22
+    uint32_t st_reg[kQPL / 2];   // step (L+1, 0 = unknown) of query r in half r & 1 of word r >> 1
+#pragma unroll
+    for (uint32_t r = 0; r < kQPL / 2; r++) st_reg[r] = 0x00010001u;
 #pragma unroll
     for (uint32_t g = 0; g < kQPL; g += kIlp) {
-        Walk W[kIlp];
+        uint32_t rng[kIlp], best[kIlp], xpk[kIlp], qa[kIlp], qb[kIlp], qc[kIlp];   // rng ~0 = unknown
         uint32_t nmax = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kIlp; u++) {
-            Walk &w = W[u];
-            w.x = q0 + tid + kMT * (g + u);
-            w.c = 0; w.best = kMinL - 1; w.bestx = 0xFFFFFFFFu; w.steps = 0; w.unk = false;
-            w.cap = 0; w.xlo = 0; w.tag = 0; w.q1 = 0; w.q2 = 0;
-            if (w.x < npos) {
-                const uint32_t i = w0 + w.x;
+            const uint32_t x = q0 + tid + kMT * (g + u);
+            rng[u] = 0; best[u] = 0; xpk[u] = x; qa[u] = qb[u] = qc[u] = 0;
+            if (x < npos) {
+                const uint32_t i = w0 + x;
                 if (i != 0 && blen - i >= 4 && !(dbg & 1u)) {
-                    w.cap = min(kMaxL, blen - i) - 1;
-                    const uint32_t h = key_mix(lds_key3(sdw, w.x));
-                    w.tag = h & 0xFFFu;
-                    w.xlo = (i > kWin ? i - kWin : 0) - w0;
-                    w.q1 = lds_ld4(sdw, w.x + 3);
-                    w.q2 = lds_ld4(sdw, w.x + 7);
-                    w.c = head[h >> 12];                       // range start
-                    w.steps = head[(h >> 12) + 1] - w.c;      // range length
-                    if (w.steps > kMaxChainSteps) { w.unk = true; w.steps = 0; }
-                    nmax = max(nmax, w.steps);
+                    const uint32_t cap = min(kMaxL, blen - i) - 1;
+                    qa[u] = lds_ld4(sdw, x);
+                    qb[u] = lds_ld4(sdw, x + 4);
+                    qc[u] = lds_ld4(sdw, x + 8);
+                    const uint32_t h = key_mix(qa[u] & 0xFFFFFFu);
+                    const uint32_t bk = h >> 12;
+                    const uint32_t lo = h16[bk], n = h16[bk + 1] - lo;
+                    xpk[u] = x | (cap << 13) | ((h & 7u) << 22);
+                    if (n > kMaxChainSteps) rng[u] = 0xFFFFFFFFu;
+                    else { rng[u] = lo | (n << 16); nmax = max(nmax, n); }
                 }
             }
         }
         for (uint32_t j = 0; j < nmax; j++) {
 #pragma unroll
             for (uint32_t u = 0; u < kIlp; u++) {
-                Walk &w = W[u];
-                if (j >= w.steps) continue;
-                const uint32_t nd = node[w.c + j];
+                if (j >= (rng[u] >> 16) || rng[u] == 0xFFFFFFFFu) continue;
+                const uint32_t nd = ent[(rng[u] & 0xFFFFu) + j];
                 const uint32_t xe = nd & 0x1FFFu;
-                if ((nd >> 13) != w.tag || xe >= w.x || xe < w.xlo) continue;
-                // common prefix with the query: bytes 0..2 equal by the key
+                const uint32_t x = xpk[u] & 0x1FFFu;
+                const uint32_t xlo = max(w0 + x, kWin) - kWin - w0;
+                if ((nd >> 13) != (xpk[u] >> 22) || xe >= x || xe < xlo) continue;
+                // bytes 0..11 of the candidate, from four aligned dwords
+                const uint32_t wb = xe >> 2, sb = xe & 3;
+                const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1], w_2 = sdw[wb + 2], w_3 = sdw[wb + 3];
+                const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa[u];
+                if (d0 & 0xFFFFFFu) continue;   // 3-tag-bit collision: different key
+                const uint32_t cap = (xpk[u] >> 13) & 0x1FFu;
                 uint32_t Lc;
-                const uint32_t a = lds_ld4(sdw, xe + 3) ^ w.q1;
-                if (a) {
-                    Lc = 3 + (__builtin_ctz(a) >> 3);
-                } else {
-                    const uint32_t bb = lds_ld4(sdw, xe + 7) ^ w.q2;
-                    if (bb) Lc = 7 + (__builtin_ctz(bb) >> 3);
-                    else Lc = (w.cap > 11 && !(dbg & 2u)) ? lds_match_len(sdw, xe, w.x, 11, w.cap) : 11;
+                if (d0) Lc = 3;
+                else {
+                    const uint32_t d1 = __builtin_amdgcn_alignbyte(w_2, w_1, sb) ^ qb[u];
+                    if (d1) Lc = 4 + (__builtin_ctz(d1) >> 3);
+                    else {
+                        const uint32_t d2 = __builtin_amdgcn_alignbyte(w_3, w_2, sb) ^ qc[u];
+                        if (d2) Lc = 8 + (__builtin_ctz(d2) >> 3);
+                        else Lc = (cap > 12 && !(dbg & 2u)) ? lds_match_len(sdw, xe, x, 12, cap) : 12;
+                    }
                 }
-                Lc = min(Lc, w.cap);
-                if (Lc > w.best || (Lc == w.best && xe < w.bestx)) { w.best = Lc; w.bestx = xe; }
+                Lc = min(Lc, cap);
+                best[u] = max(best[u], (Lc << 13) | (8191u - xe));
             }
         }
 #pragma unroll
         for (uint32_t u = 0; u < kIlp; u++) {
-            Walk &w = W[u];
+            const uint32_t x = xpk[u] & 0x1FFFu;
             uint32_t st = 1, res = 0;
-            if (w.x < npos) {
-                if (w.unk) { res = kUnknown; st = 0; s_unknown = 1; }
-                else if (w.best >= kMinL) { res = m_pack(w.best, w.x - w.bestx); st = w.best + 1; }
-                if (res) m[bstart + w0 + w.x] = res;   // m is stored only where mbits says so
+            if (x < npos) {
+                const uint32_t Lb = best[u] >> 13, xb = 8191u - (best[u] & 0x1FFFu);
+                if (rng[u] == 0xFFFFFFFFu) { res = kUnknown; st = 0; s_unknown = 1; }
+                else if (Lb >= kMinL) { res = m_pack(Lb, x - xb); st = Lb + 1; }
+                if (res) m[bstart + w0 + x] = res;   // m is stored only where mbits says so
             }
             // the wave's 64 lanes hold 64 consecutive positions = one mbits word
             const uint64_t mb = __ballot(res != 0);
             const uint32_t xw = q0 + (tid & ~63u) + kMT * (g + u);
             if ((tid & 63) == 0 && xw < npos) mbits[(uint64_t)b * L.wpb + ((w0 + xw) >> 6)] = mb;
-            st_reg[g + u] = st;
+            const uint32_t q = g + u;
+            st_reg[q >> 1] = (q & 1) ? ((st_reg[q >> 1] & 0xFFFFu) | (st << 16)) : ((st_reg[q >> 1] & 0xFFFF0000u) | st);
         }
     }
-    __syncthreads();   // head[] is dead from here on
+    __syncthreads();   // the search region is dead from here on
 
     uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
     uint32_t *ti = tinfo + 8ull * blockIdx.x;
@@ -212,12 +238,12 @@ __global__ __launch_bounds__(kMT) void k_match(const uint8_t *__restrict__ in, L
     }
 
     // ---- 4. tile-local greedy parse ----
-    uint16_t *step = (uint16_t *)head;                 // 8 KB
-    uint32_t *Gs = head + kTile / 2;                   // kMT + 1 entries
+    uint16_t *step = (uint16_t *)region;               // 8 KB
+    uint32_t *Gs = region + kTile / 2;                 // kMT + 1 entries
     uint32_t *Xs = Gs + kMT + 1;
     uint32_t *Vs = Xs + kMT;
 #pragma unroll
-    for (uint32_t r = 0; r < kQPL; r++) step[tid + kMT * r] = (uint16_t)st_reg[r];
+    for (uint32_t r = 0; r < kQPL; r++) step[tid + kMT * r] = (uint16_t)(st_reg[r >> 1] >> (16 * (r & 1)));
     __syncthreads();
     const uint32_t s = t0 + tid * kSeg;
     const uint32_t se = min(s + kSeg, t1);
