@@ -98,7 +98,9 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages):
     dt = time.perf_counter() - t0
     ctx.set_profiling(False)
     if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64)
+        if dist.get_backend() != "gloo":
+            tt = tt.to(dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     out_len = ctx.read_out_len()   # segment size of the timed steps (device word)
@@ -129,29 +131,32 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages):
 
 
 def allgather_concat(d_out, seg_len, world, dev, dist):
-    """RCCL all-gather of the per-rank segments (sizes first, then segments padded
-    to the max), assembled in rank order on every rank."""
+    """RCCL all-gather of the per-rank segments (my_compress_amd.dist): sizes,
+    then segments padded to the largest, assembled in rank order on every rank.
+    With the gloo backend (rehearsal) the segments travel through host memory."""
     import torch
 
-    sizes = torch.tensor([seg_len], dtype=torch.int64, device=dev)
-    all_sizes = torch.empty(world, dtype=torch.int64, device=dev)
+    from my_compress_amd import dist as fdist
+
+    on_host = dist.get_backend() == "gloo"
     dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    dist.all_gather_into_tensor(all_sizes, sizes)
-    szs = [int(x) for x in all_sizes.cpu()]
-    mx = max(szs)
-    recv = torch.empty(world * mx, dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(recv, d_out[:mx])
-    whole = torch.cat([recv[r * mx: r * mx + szs[r]] for r in range(world)])
+    seg = d_out[:seg_len]
+    if on_host:
+        seg = seg.cpu()
+    whole = fdist.concat_segments(seg, dist)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+    tt = torch.tensor([dt], dtype=torch.float64)
+    if not on_host:
+        tt = tt.to(dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
     total = int(whole.numel())
-    del recv, whole
-    return {"kind": "allgather", "ms": dt * 1e3, "bytes": total, "GBps_per_rank_recv": (total - seg_len) / dt / 1e9}
+    del whole
+    return {"kind": "allgather" + ("(gloo,host)" if on_host else "(rccl)"), "ms": dt * 1e3, "bytes": total,
+            "GBps_per_rank_recv": (total - seg_len) / dt / 1e9}
 
 
 def cpu_baseline(kind, seed, block, threads=16, nblocks=32):
@@ -217,6 +222,7 @@ def main():
     ap.add_argument("--block", type=int, default=1 << 20)
     ap.add_argument("--no-text", action="store_true", help="skip the text leg")
     ap.add_argument("--concat", default="allgather", choices=["allgather", "none"])
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
@@ -227,13 +233,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device(f"cuda:{local}")
+    # FCX_BENCH_SAME_DEVICE=1: every rank on cuda:0 (rehearsing N>1 on a one-GPU box, with --dist-backend gloo)
+    dev = torch.device("cuda:0" if os.environ.get("FCX_BENCH_SAME_DEVICE") == "1" else f"cuda:{local}")
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist_
 
-        dist_.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist_.init_process_group("nccl", device_id=dev)
+        else:
+            dist_.init_process_group("gloo")
         dist = dist_
     seeds = {"rand": 4, "text": 3, "runs": 5, "zeros": 0}
     main_res, concat = run_leg(args.kind, seeds[args.kind], args, rank, world, dev, dist, True)

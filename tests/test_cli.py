@@ -1,0 +1,70 @@
+"""The my_compress CLI (main(), my_compress.cpp:3726-4213): same flags, default
+output ./out, same byte stream.  Decompress runs on the host decoder (CPU test);
+compress runs on the GPU (gpu test) and fails loudly without one."""
+import hashlib
+import os
+import subprocess
+
+import pytest
+
+import inputs
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "my_compress_amd", "bin", "my_compress")
+
+
+def run(args, cwd):
+    return subprocess.run([CLI] + args, cwd=cwd, capture_output=True, text=True, timeout=600)
+
+
+def test_cli_decompresses_reference_streams(tmp_path, golden):
+    for case in golden["cases"]:
+        if case["name"] not in ("text_s7_300000_b4096", "mosaic_s1_b65536", "kat30", "tiny_17"):
+            continue
+        data = inputs.make(case)
+        blob = oracle.compress_file(data, case["block"])
+        (tmp_path / "in.fcx").write_bytes(blob)
+        r = run(["-i", "in.fcx", "-o", "plain"], tmp_path)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "SUCCESS" in r.stdout
+        assert (tmp_path / "plain").read_bytes() == data
+
+
+def test_cli_rejects_foreign_stream_and_lz78(tmp_path):
+    (tmp_path / "junk").write_bytes(b"NOTFCX" * 10)
+    assert run(["-i", "junk", "-o", "x"], tmp_path).returncode != 0
+    (tmp_path / "plain").write_bytes(b"hello")
+    r = run(["-i", "plain", "-o", "x", "-c", "lz78"], tmp_path)
+    assert r.returncode != 0 and "scope" in r.stderr
+
+
+def test_cli_compress_fails_loudly_without_gpu(tmp_path):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    (tmp_path / "plain").write_bytes(b"hello hello hello hello")
+    r = run(["-i", "plain", "-o", "x", "-c", "lz77"], tmp_path)
+    assert r.returncode != 0
+    assert "GPU" in r.stderr or "HIP" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_compress_matches_reference(tmp_path, golden):
+    for case in golden["cases"]:
+        if case["name"] not in ("text_s1_1048576_b1048576", "text_plus_partial", "A_x100000", "mosaic_s2_b1048576"):
+            continue
+        data = inputs.make(case)
+        (tmp_path / "plain").write_bytes(data)
+        args = ["-i", "plain", "-c", "lz77"]
+        if case["block"] != 1 << 20:
+            args += ["-b", str(case["block"])]
+        r = run(args, tmp_path)   # default output ./out (my_compress.cpp:4040-4042)
+        assert r.returncode == 0, r.stderr
+        out = (tmp_path / "out").read_bytes()
+        assert hashlib.sha256(out).hexdigest() == case["out_sha256"], case["name"]
+        r = run(["-i", "out", "-o", "back"], tmp_path)
+        assert r.returncode == 0
+        if case["name"] != "A_x100000":   # single-symbol chars stream decodes as zeros (reference behaviour)
+            assert (tmp_path / "back").read_bytes() == data
