@@ -47,9 +47,9 @@ int hip_fail(hipError_t e, const char *what) {
 
 inline uint32_t round16(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
 
-const char *kStageNames[] = {"memset", "match",        "stitch",      "emit", "hist",   "tree",
-                             "bitcount", "block_layout", "scan_blocks", "zero", "encode", "headers"};
-constexpr int kNumStages = 12;
+const char *kStageNames[] = {"memset",       "match",       "stitch", "emit",   "hist",   "tree",
+                             "block_layout", "scan_blocks", "zero",   "encode", "headers"};
+constexpr int kNumStages = 11;
 
 Layout make_layout(uint64_t n, uint32_t B) {
     Layout L;
@@ -88,7 +88,8 @@ struct fcx_ctx {
     uint64_t *fp = nullptr;            // per tile: fast-path record (k_resolve)
     BlockInfo *binfo = nullptr;
     uint8_t *s[kStreams] = {nullptr, nullptr, nullptr, nullptr};
-    uint32_t *hist = nullptr, *ctab = nullptr, *chunk_bits = nullptr;
+    uint32_t *hist = nullptr;          // per chunk: 256-bin histogram
+    uint32_t *ctab = nullptr, *chunk_bits = nullptr;   // code table; per chunk: starting bit offset
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
     uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits
@@ -146,7 +147,7 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     if ((r = dalloc(&c->binfo, sizeof(BlockInfo) * nb, "binfo"))) return r;
     for (uint32_t s = 0; s < kStreams; s++)
         if ((r = dalloc(&c->s[s], (uint64_t)L.sstride[s] * nb + 64, "stream"))) return r;
-    if ((r = dalloc(&c->hist, 4ull * 256 * kStreams * nb, "hist"))) return r;
+    if ((r = dalloc(&c->hist, 4ull * 256 * L.cpb_total * nb, "hist"))) return r;
     if ((r = dalloc(&c->ctab, 4ull * 256 * kStreams * nb, "ctab"))) return r;
     if ((r = dalloc(&c->ltab, 256ull * kStreams * nb, "ltab"))) return r;
     if ((r = dalloc(&c->hhdr, (uint64_t)kHuffHdrStride * kStreams * nb, "hhdr"))) return r;
@@ -290,7 +291,6 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     HIP_TRY(hipMemsetAsync(c->s[0], 0, (uint64_t)L.sstride[0] * L.nblocks, st));
     HIP_TRY(hipMemsetAsync(c->s[2], 0, (uint64_t)L.sstride[2] * L.nblocks, st));
     HIP_TRY(hipMemsetAsync(c->s[3], 0, (uint64_t)L.sstride[3] * L.nblocks, st));
-    HIP_TRY(hipMemsetAsync(c->hist, 0, 4ull * 256 * kStreams * L.nblocks, st));
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
     launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, st);
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));

@@ -13,21 +13,24 @@
 // per (block, stream), then serialises the tree (1013-1066) and the code table:
 // code = root->leaf path, left = 0, root decision in bit 0 (LSB-first, 869-924).
 //
-//   k_hist         256-bin histograms per (block, stream), per-wave LDS bins
-//   k_tree         tree + header bytes + code table + code-word count W
-//   k_bitcount     code bits per 8192-symbol chunk
-//   k_block_layout chunk bit offsets, record layout and size per block
+//   k_hist         256-bin histogram of every 8192-symbol chunk (per-wave LDS
+//                  bins, runs of equal bytes counted in registers first)
+//   k_tree         sums a stream's chunk histograms, builds the tree, header
+//                  bytes, code table, W, and every chunk's starting bit offset
+//                  (chunk histogram . code lengths) - no second pass over the data
+//   k_block_layout record layout and size per block
 //   k_scan_blocks  record offsets across the shard (+ capacity check)
 //   k_zero         zero the output bytes the encoder ORs into
-//   k_encode       pack codes of a chunk into LDS words, store them at the
-//                  record's (unaligned) byte offset: interior words plain,
-//                  chunk-edge words atomicOr
+//   k_encode       each lane packs its 32 codes into whole words (LDS atomics only
+//                  for the two words it shares with neighbours); the chunk's words
+//                  are stored at the record's (unaligned) byte offset: interior
+//                  words plain, chunk-edge words atomicOr
 //   k_headers      lengths, counts and tree headers of every record
 #include "fcx_device.h"
 
 namespace fcx {
 
-constexpr uint32_t kErrCodeLen = 1u, kErrBitCount = 2u, kErrCapacity = 4u;
+constexpr uint32_t kErrCodeLen = 1u, kErrCapacity = 4u;
 
 __device__ inline bool stream_active(const BlockInfo &bi, uint32_t s) {
     if (s == 0) return bi.slen[0] > 1;   // flags are Huffman-coded only when > 1 byte
@@ -42,6 +45,19 @@ __device__ inline void chunk_of(const Layout &L, uint32_t r, uint32_t &s, uint32
 }
 
 // ---------------------------------------------------------------------------
+__device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32_t i1, uint32_t *out32 /*8 words*/) {
+    // loads the (up to) 32 symbols [i0, i1) as 8 words, masked past i1
+    const uint32_t n = i1 > i0 ? i1 - i0 : 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) out32[q] = (4 * q < n) ? w4[(i0 >> 2) + q] : 0u;
+    return n;
+}
+
+__device__ inline const uint8_t *stream_base(const Layout &L, uint32_t s, uint32_t b, const uint8_t *s0,
+                                             const uint8_t *s1, const uint8_t *s2, const uint8_t *s3) {
+    return (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
+}
+
 __global__ __launch_bounds__(256) void k_hist(Layout L, const BlockInfo *__restrict__ binfo,
                                               const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
                                               const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
@@ -56,24 +72,32 @@ __global__ __launch_bounds__(256) void k_hist(Layout L, const BlockInfo *__restr
     const uint32_t len = bi.slen[s], c0 = c * kChunk;
     if (c0 >= len) return;
     const uint32_t c1 = min(len, c0 + kChunk);
-    const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
-    const uint32_t *w4 = (const uint32_t *)base;
     for (uint32_t x = tid; x < 1024; x += 256) (&h[0][0])[x] = 0;
     __syncthreads();
-    for (uint32_t wi = (c0 >> 2) + tid; 4 * wi < c1; wi += 256) {
-        const uint32_t v = w4[wi];
-        const uint32_t nb = min(4u, c1 - 4 * wi);
-        for (uint32_t q = 0; q < nb; q++) atomicAdd(&h[wv][(v >> (8 * q)) & 0xFF], 1u);
+    // each lane counts a strip of 32 consecutive symbols, runs of one byte value first
+    const uint32_t i0 = c0 + 32 * tid, i1 = min(c1, i0 + 32);
+    uint32_t sym[8];
+    const uint32_t n = chunk_symbols((const uint32_t *)stream_base(L, s, b, s0, s1, s2, s3), i0, i1, sym);
+    uint32_t cur = sym[0] & 0xFF, run = 0;
+    for (uint32_t q = 0; q < n; q++) {
+        const uint32_t v = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
+        if (v != cur) {
+            atomicAdd(&h[wv][cur], run);
+            cur = v;
+            run = 0;
+        }
+        run++;
     }
+    if (run) atomicAdd(&h[wv][cur], run);
     __syncthreads();
-    const uint32_t tot = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
-    if (tot) atomicAdd(&hist[(b * kStreams + s) * 256 + tid], tot);
+    hist[(uint64_t)blockIdx.x * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_tree(const uint32_t *__restrict__ hist, BlockInfo *__restrict__ binfo,
-                                             uint32_t *__restrict__ ctab, uint8_t *__restrict__ ltab,
-                                             uint8_t *__restrict__ hhdr, uint32_t *__restrict__ err) {
+__global__ __launch_bounds__(64) void k_tree(Layout L, const uint32_t *__restrict__ hist,
+                                             BlockInfo *__restrict__ binfo, uint32_t *__restrict__ ctab,
+                                             uint8_t *__restrict__ ltab, uint8_t *__restrict__ hhdr,
+                                             uint32_t *__restrict__ chunk_off, uint32_t *__restrict__ err) {
     __shared__ uint32_t w[256], sw[256], ss[256];
     __shared__ uint32_t iw[256], il[256], ir[256], par[512];
     const uint32_t lane = threadIdx.x;
@@ -84,12 +108,19 @@ __global__ __launch_bounds__(64) void k_tree(const uint32_t *__restrict__ hist, 
         return;
     }
     const uint32_t hb = (b * kStreams + s) * 256;
+    uint32_t r0 = 0;
+    for (uint32_t q = 0; q < s; q++) r0 += L.cpb[q];
+    const uint32_t nch = (bi.slen[s] + kChunk - 1) / kChunk;
+    const uint32_t *hc = hist + ((uint64_t)b * L.cpb_total + r0) * 256;   // this stream's chunk histograms
+    uint32_t acc[4] = {0, 0, 0, 0};
+    for (uint32_t c = 0; c < nch; c++)
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) acc[q] += hc[c * 256 + lane + 64 * q];
     uint32_t real = 0;
 #pragma unroll
     for (uint32_t q = 0; q < 4; q++) {
-        const uint32_t v = hist[hb + lane + 64 * q];
-        w[lane + 64 * q] = v;
-        real += (uint32_t)__popcll(__ballot(v != 0));
+        w[lane + 64 * q] = acc[q];
+        real += (uint32_t)__popcll(__ballot(acc[q] != 0));
     }
     __syncthreads();
     // stable sort of the leaves by (weight, symbol): rank = number of smaller keys
@@ -127,7 +158,7 @@ __global__ __launch_bounds__(64) void k_tree(const uint32_t *__restrict__ hist, 
     }
     __syncthreads();
     const uint32_t root = 256 + nint - 1;
-    uint64_t bits = 0;
+    uint32_t myl[4];
 #pragma unroll
     for (uint32_t q = 0; q < 4; q++) {
         const uint32_t sym = lane + 64 * q;
@@ -144,9 +175,18 @@ __global__ __launch_bounds__(64) void k_tree(const uint32_t *__restrict__ hist, 
         }
         ctab[hb + sym] = code;
         ltab[hb + sym] = (uint8_t)len;
-        bits += (uint64_t)w[sym] * len;
+        myl[q] = len;
     }
-    bits = wave_sum_u64(bits);
+    // starting bit of every chunk: chunk histogram . code lengths, scanned in chunk order
+    uint64_t bits = 0;
+    for (uint32_t c = 0; c < nch; c++) {
+        uint32_t part = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) part += hc[c * 256 + lane + 64 * q] * myl[q];
+        part = wave_sum_u32(part);
+        if (lane == 0) chunk_off[(uint64_t)b * L.cpb_total + r0 + c] = (uint32_t)bits;
+        bits += part;
+    }
     // header: [u8 ts][ceil(2ts/8) B internal-child bitmap][ts x (u8 l, u8 r)]
     const uint32_t ts = nint, nbm = (2 * ts + 7) / 8;
     uint8_t *hdr = hhdr + (uint64_t)(b * kStreams + s) * kHuffHdrStride;
@@ -174,45 +214,6 @@ __global__ __launch_bounds__(64) void k_tree(const uint32_t *__restrict__ hist, 
 }
 
 // ---------------------------------------------------------------------------
-__device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32_t i1, uint32_t *out32 /*8 words*/) {
-    // loads the (up to) 32 symbols [i0, i1) as 8 words, masked past i1
-    const uint32_t n = i1 > i0 ? i1 - i0 : 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 8; q++) out32[q] = (4 * q < n) ? w4[(i0 >> 2) + q] : 0u;
-    return n;
-}
-
-__global__ __launch_bounds__(256) void k_bitcount(Layout L, const BlockInfo *__restrict__ binfo,
-                                                  const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
-                                                  const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
-                                                  const uint8_t *__restrict__ ltab, uint32_t *__restrict__ chunk_bits) {
-    __shared__ uint32_t lt[256];
-    __shared__ uint32_t red[4];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t b = blockIdx.x / L.cpb_total, r = blockIdx.x % L.cpb_total;
-    uint32_t s, c;
-    chunk_of(L, r, s, c);
-    const BlockInfo &bi = binfo[b];
-    const uint32_t len = bi.slen[s], c0 = c * kChunk;
-    if (!stream_active(bi, s) || c0 >= len) {
-        if (tid == 0) chunk_bits[blockIdx.x] = 0;
-        return;
-    }
-    const uint32_t c1 = min(len, c0 + kChunk);
-    lt[tid] = ltab[(b * kStreams + s) * 256 + tid];
-    __syncthreads();
-    const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
-    const uint32_t i0 = c0 + 32 * tid, i1 = min(c1, i0 + 32);
-    uint32_t sym[8];
-    const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
-    uint32_t nb = 0;
-    for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
-    nb = wave_sum_u32(nb);
-    if ((tid & 63) == 0) red[tid >> 6] = nb;
-    __syncthreads();
-    if (tid == 0) chunk_bits[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-
 // record layout of one block: offsets relative to the record start
 struct RecLayout {
     uint32_t hdr_rel[kStreams];    // tree header (or raw flag bytes for s=0 when not Huffman-coded)
@@ -244,29 +245,13 @@ __device__ inline RecLayout record_layout(const BlockInfo &bi) {
     return R;
 }
 
-__global__ __launch_bounds__(64) void k_block_layout(Layout L, BlockInfo *__restrict__ binfo,
-                                                     uint32_t *__restrict__ chunk_bits, uint32_t *__restrict__ err) {
-    const uint32_t lane = threadIdx.x, b = blockIdx.x;
+__global__ __launch_bounds__(64) void k_block_layout(uint32_t nblocks, BlockInfo *__restrict__ binfo) {
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= nblocks) return;
     BlockInfo &bi = binfo[b];
-    if (lane < kStreams) {
-        const uint32_t s = lane;
-        uint32_t r0 = 0;
-        for (uint32_t q = 0; q < s; q++) r0 += L.cpb[q];
-        uint32_t run = 0;
-        for (uint32_t c = 0; c < L.cpb[s]; c++) {
-            uint32_t &cb = chunk_bits[(uint64_t)b * L.cpb_total + r0 + c];
-            const uint32_t v = cb;
-            cb = run;                       // -> exclusive bit offset of the chunk
-            run += v;
-        }
-        if (stream_active(bi, s) && (run + 31) / 32 != bi.nwords[s]) atomicOr(err, kErrBitCount);
-    }
-    __syncthreads();
-    if (lane == 0) {
-        const RecLayout R = record_layout(bi);
-        for (uint32_t s = 0; s < kStreams; s++) bi.words_rel[s] = R.words_rel[s];
-        bi.rec_bytes = R.rec_bytes;
-    }
+    const RecLayout R = record_layout(bi);
+    for (uint32_t s = 0; s < kStreams; s++) bi.words_rel[s] = R.words_rel[s];
+    bi.rec_bytes = R.rec_bytes;
 }
 
 __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t nblocks, const BlockInfo *__restrict__ binfo,
@@ -359,14 +344,18 @@ __global__ __launch_bounds__(256) void k_encode(Layout L, const BlockInfo *__res
     const uint32_t nw = (sh0 + ctot + 31) >> 5;
     for (uint32_t x = tid; x < nw; x += 256) ws[x] = 0;
     __syncthreads();
-    uint32_t pos = sh0 + tb, wi = pos >> 5, ap = pos & 31;
+    // this lane's codes cover bits [p0, p1) of the staging words; whole words inside
+    // that range are this lane's alone (plain LDS stores), the two end words are shared
+    const uint32_t p0 = sh0 + tb, p1 = p0 + nb;
+    uint32_t wi = p0 >> 5, ap = p0 & 31;
     uint64_t acc = 0;
     for (uint32_t q = 0; q < n; q++) {
         const uint32_t sy = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
         acc |= (uint64_t)ct[sy] << ap;
         ap += lt[sy];
-        while (ap >= 32) {
-            atomicOr(&ws[wi], (uint32_t)acc);
+        if (ap >= 32) {
+            if (32 * wi >= p0 && 32 * wi + 32 <= p1) ws[wi] = (uint32_t)acc;
+            else atomicOr(&ws[wi], (uint32_t)acc);
             acc >>= 32;
             ap -= 32;
             wi++;
@@ -416,27 +405,26 @@ __global__ __launch_bounds__(64) void k_headers(const BlockInfo *__restrict__ bi
 
 // ---------------------------------------------------------------------------
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
-                    uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_bits,
+                    uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_off,
                     uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
                     hipEvent_t *ev) {
     const uint32_t nchunks = L.nblocks * L.cpb_total;
     hipLaunchKernelGGL(k_hist, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, hist);
     if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(64), 0, st, hist, binfo, ctab, ltab, hhdr, err);
+    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(64), 0, st, L, hist, binfo, ctab, ltab, hhdr,
+                       chunk_off, err);
     if (ev) (void)hipEventRecord(ev[1], st);
-    hipLaunchKernelGGL(k_bitcount, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, ltab, chunk_bits);
+    hipLaunchKernelGGL(k_block_layout, dim3((L.nblocks + 63) / 64), dim3(64), 0, st, L.nblocks, binfo);
     if (ev) (void)hipEventRecord(ev[2], st);
-    hipLaunchKernelGGL(k_block_layout, dim3(L.nblocks), dim3(64), 0, st, L, binfo, chunk_bits, err);
-    if (ev) (void)hipEventRecord(ev[3], st);
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, L.nblocks, binfo, blk_off, total, cap, err);
-    if (ev) (void)hipEventRecord(ev[4], st);
+    if (ev) (void)hipEventRecord(ev[3], st);
     hipLaunchKernelGGL(k_zero, dim3(2048), dim3(256), 0, st, out, total, err);
-    if (ev) (void)hipEventRecord(ev[5], st);
-    hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, chunk_bits,
+    if (ev) (void)hipEventRecord(ev[4], st);
+    hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, chunk_off,
                        blk_off, out, err);
-    if (ev) (void)hipEventRecord(ev[6], st);
+    if (ev) (void)hipEventRecord(ev[5], st);
     hipLaunchKernelGGL(k_headers, dim3(L.nblocks), dim3(64), 0, st, binfo, s0, L.sstride[0], hhdr, blk_off, out, err);
-    if (ev) (void)hipEventRecord(ev[7], st);
+    if (ev) (void)hipEventRecord(ev[6], st);
 }
 
 }  // namespace fcx
