@@ -216,10 +216,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                 const uint32_t Lb = best[u] >> 13, xb = 8191u - (best[u] & 0x1FFFu);
                 if (rng[u] == 0xFFFFFFFFu) { res = kUnknown; st = 0; s_unknown = 1; }
                 else if (Lb >= kMinL) { res = m_pack(Lb, x - xb); st = Lb + 1; }
-                if (res) m[bstart + w0 + x] = res;   // m is stored only where mbits says so
             }
-            // the wave's 64 lanes hold 64 consecutive positions = one mbits word
+            // the wave's 64 lanes hold 64 consecutive positions = one mbits word; m is
+            // stored (whole 256-B rows, zeros included) only by waves that found a match
             const uint64_t mb = __ballot(res != 0);
+            if (mb && x < npos) m[bstart + w0 + x] = res;
             const uint32_t xw = q0 + (tid & ~63u) + kMT * (g + u);
             if ((tid & 63) == 0 && xw < npos) mbits[(uint64_t)b * L.wpb + ((w0 + xw) >> 6)] = mb;
             const uint32_t q = g + u;

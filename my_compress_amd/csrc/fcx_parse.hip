@@ -457,9 +457,19 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     const uint32_t *mt = m + bstart + s;
     uint32_t mm[16];
     uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0};
+    if (rd && ((uintptr_t)mt & 15) == 0) {   // whole 64-B row as four 16-B loads
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint4 w4 = ((const uint4 *)mt)[q];
+            mm[4 * q] = w4.x; mm[4 * q + 1] = w4.y; mm[4 * q + 2] = w4.z; mm[4 * q + 3] = w4.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < 16; q++) mm[q] = ((rd >> q) & 1u) ? mt[q] : 0u;
+    }
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
-        mm[q] = ((rd >> q) & 1u) ? mt[q] : 0u;
+        mm[q] = ((rd >> q) & 1u) ? mm[q] : 0u;
         const uint32_t Lq = m_len(mm[q]);
         if (((bits >> q) & 1u) && Lq) { v[1]++; v[2] += (Lq >> 2) + 3; }
     }

