@@ -102,6 +102,17 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// inclusive running maximum across the 64 lanes
+__device__ inline uint32_t wave_incl_max(uint32_t v) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= (uint32_t)o) v = max(v, t);
+    }
+    return v;
+}
+
 // unaligned 4-byte little-endian read from an LDS byte image backed by u32 words
 __device__ inline uint32_t lds_ld4(const uint32_t *w, uint32_t pos) {
     uint32_t lo = w[pos >> 2], hi = w[(pos >> 2) + 1];
@@ -125,5 +136,93 @@ __device__ inline uint32_t lds_match_len(const uint32_t *w, uint32_t a, uint32_t
 }
 
 __device__ inline uint32_t hash3(uint32_t key) { return (key * 2654435761u) >> (32 - kHashBits); }
+
+// ---- exact match over the run decomposition (dense windows: zeros, runs) ----
+// Runs of equal bytes in an LDS byte image are described by a boundary bitmap
+// (bit y: y == 0 or byte y != byte y-1; plus a sentinel bit at the image end),
+// per-32-bit-word prefix counts, and the run table rt[k] = start | byte << 16
+// (the sentinel entry carries byte 0x100).  For a query x with own run ending at
+// e (r = e - x remaining bytes) and an earlier run k' of the same byte with A
+// bytes available inside the window (from sp = max(start, xlo) to its end ep):
+//   A <  r : the common prefix at sp is A (ep holds another byte, x + A does not);
+//   A >= r : every j with ep - j > r gives exactly r (x + r holds another byte),
+//            j* = ep - r gives r + ext, ext = common prefix of ep and e;
+// candidates inside the own run give r.  Scanning runs left to right with a
+// strict > keeps the leftmost maximum, which is the reference's choice
+// (my_compress.cpp:1446-1514; SURVEY.md §0 finding 3).
+constexpr uint32_t kRunBudget = 512;       // runs per window before the position stays "unknown"
+constexpr uint32_t kRunTile = 1024;        // image runs up to which a tile skips the bucket search
+
+__device__ inline uint32_t run_rank(const uint32_t *bm, const uint16_t *prc, uint32_t y) {
+    // number of run boundaries at positions <= y
+    const uint32_t sh = y & 31;
+    const uint32_t msk = sh == 31 ? 0xFFFFFFFFu : ((2u << sh) - 1u);
+    return prc[y >> 5] + (uint32_t)__builtin_popcount(bm[y >> 5] & msk);
+}
+
+// m of image position x (block position x + base), window from image position xlo,
+// length cap; ok = false when the window holds more than kRunBudget runs.
+__device__ inline uint32_t run_match(const uint32_t *img, const uint32_t *bm, const uint16_t *prc, const uint32_t *rt,
+                                     uint32_t x, uint32_t xlo, uint32_t cap, bool &ok) {
+    const uint32_t ko = run_rank(bm, prc, x) - 1;
+    const uint32_t klo = run_rank(bm, prc, xlo) - 1;
+    if (ko - klo > kRunBudget) { ok = false; return 0; }
+    ok = true;
+    const uint32_t own = rt[ko];
+    const uint32_t c = own >> 16;
+    const uint32_t e = rt[ko + 1] & 0xFFFFu;
+    const uint32_t r = e - x;
+    const bool big = r > cap;     // every same-byte candidate reaches min(A, cap)
+    uint32_t bestL = 0, bestj = x;
+    const uint32_t vb0 = rt[ko + 1];   // the run after the own run (query side of ext)
+    bool done = false;
+    uint32_t cur = rt[klo];
+    for (uint32_t kk = klo; kk < ko && !done; kk += 4) {
+        // four run-table entries in flight per step (rt holds >= 4 entries past the sentinel)
+        const uint32_t v[5] = {cur, rt[kk + 1], rt[kk + 2], rt[kk + 3], rt[kk + 4]};
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            if (done || kk + u >= ko || (v[u] >> 16) != c) continue;
+            const uint32_t sp = max(v[u] & 0xFFFFu, xlo), ep = v[u + 1] & 0xFFFFu;
+            const uint32_t A = ep - sp;
+            uint32_t Lc, j = sp;
+            if (big) Lc = min(A, cap);
+            else if (A < r) Lc = A;
+            else {
+                // ext at run granularity: equal (byte, length) runs extend it, the first
+                // run that differs in length adds the shorter length and ends it.  The
+                // query side meets the image end (sentinel) only past the cap.
+                uint32_t ext = 0;
+                if (r < cap) {
+                    const uint32_t lim = cap - r;
+                    uint32_t ka = kk + u + 1, kb = ko + 1, va = v[u + 1], vb = vb0;
+                    for (;;) {
+                        if ((va >> 16) != (vb >> 16)) break;
+                        const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
+                        const uint32_t la = (na & 0xFFFFu) - (va & 0xFFFFu), lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
+                        if (la != lb) { ext += min(la, lb); break; }
+                        ext += la;
+                        if (ext >= lim) break;
+                        ka++; kb++; va = na; vb = nb;
+                    }
+                    ext = min(ext, lim);
+                }
+                Lc = min(r + ext, cap);
+                if (ext) j = ep - r;
+            }
+            if (Lc > bestL) {
+                bestL = Lc; bestj = j;
+                done = bestL >= cap;
+            }
+        }
+        cur = v[4];
+    }
+    const uint32_t sp = max(own & 0xFFFFu, xlo);
+    if (bestL < cap && sp < x) {
+        const uint32_t Lc = big ? cap : r;
+        if (Lc > bestL) { bestL = Lc; bestj = sp; }
+    }
+    return bestL >= kMinL ? m_pack(bestL, x - bestj) : 0u;
+}
 
 }  // namespace fcx

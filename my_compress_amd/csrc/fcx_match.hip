@@ -45,8 +45,152 @@ constexpr uint32_t kHeadWords = (1u << kHashBits) / 2 + 4;                 // u1
 constexpr uint32_t kEntWords = kWinPos / 2;                                 // u16 entries
 constexpr uint32_t kRegionWords = kHeadWords + kEntWords > kTile / 2 + 3 * kMT + 1
                                       ? kHeadWords + kEntWords : kTile / 2 + 3 * kMT + 1;
+// dense-window phase (run table) inside the same region
+constexpr uint32_t kRunBmWords = 208;                // 6656 bitmap positions >= kTileBytes + 1, 13 x kMT
+constexpr uint32_t kRunListWords = 2 * 64 * kWaves;   // per-wave candidate lists (se, ext)
+constexpr uint32_t kRunTableCap = kRegionWords - (kTile / 2 + kRunBmWords + kRunBmWords / 2 + 2 + kRunListWords) - 4;  // 4 spare
+static_assert(32 * kRunBmWords >= kTileBytes + 1 && (32 * kRunBmWords) % kMT == 0, "run bitmap");
+static_assert(kRunBmWords <= 4 * 64, "prefix scan spans four waves");
+static_assert(kRunTableCap >= 1536, "run table");
 
 __device__ inline uint32_t key_mix(uint32_t key) { return (key * 0x9E3779B1u) & 0xFFFFFFu; }  // bijective mod 2^24
+
+// ---- 3b. dense windows (zeros, runs): the positions the bucket search left
+// "unknown" get their exact match from the run table (run_match, fcx_device.h).
+// Kept out of line so its registers do not weigh on the search loop; it runs
+// only in tiles that have unknown positions.  mx = m of image position 0, ilen =
+// block length - image base, w0 = image base in the block.  mbx (whole-tile mode,
+// no bucket search ran): mbits of image position 0, written here per 64 positions.
+__device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, uint16_t *step, uint32_t *s_red,
+                                         uint32_t *s_unknown, uint32_t *mx, uint64_t *mbx, uint32_t q0, uint32_t npos,
+                                         uint32_t nload, uint32_t ilen, uint32_t w0) {
+    const uint32_t tid = threadIdx.x;
+    uint32_t *rbm = region + kTile / 2;                       // boundary bitmap, kRunBmWords
+    uint16_t *prc = (uint16_t *)(rbm + kRunBmWords);          // prefix counts per bitmap word
+    uint32_t *rt = rbm + kRunBmWords + kRunBmWords / 2 + 2 + kRunListWords;   // run table
+    // bitmap by ballot: a wave's 64 lanes cover 64 consecutive image positions
+    for (uint32_t y0 = 0; y0 < 32 * kRunBmWords; y0 += kMT) {
+        const uint32_t y = y0 + tid;
+        const bool bit = y == nload || (y < nload && (y == 0 || lds_ld1(sdw, y) != lds_ld1(sdw, y - 1)));
+        const uint64_t bal = __ballot(bit);
+        if ((tid & 63) == 0) { rbm[y >> 5] = (uint32_t)bal; rbm[(y >> 5) + 1] = (uint32_t)(bal >> 32); }
+    }
+    __syncthreads();
+    // exclusive prefix counts (kRunBmWords <= 4 waves of lanes)
+    const uint32_t pc = tid < kRunBmWords ? (uint32_t)__builtin_popcount(rbm[tid]) : 0u;
+    const uint32_t inc = wave_incl_scan(pc);
+    if ((tid & 63) == 63) s_red[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t pre = inc - pc;
+    for (uint32_t w = 0; w < (tid >> 6); w++) pre += s_red[w];
+    const uint32_t nruns = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    if (tid < kRunBmWords) prc[tid] = (uint16_t)pre;
+    if (nruns <= kRunTableCap && tid < kRunBmWords)
+        for (uint32_t v = rbm[tid], o = pre; v; v &= v - 1, o++) {
+            const uint32_t y = 32 * tid + __builtin_ctz(v);
+            rt[o] = y | (y < nload ? lds_ld1(sdw, y) << 16 : 0x1000000u);
+        }
+    if (tid == 0) *s_unknown = 0;
+    __syncthreads();
+    // Evaluation, one chunk of 64 consecutive positions per wave step.  The chunk's
+    // positions fall into a few own runs; for each, the wave scans the window's
+    // runs one per lane, keeps those of the own run's byte (with ext, the run-level
+    // common prefix after them, precomputed up to kMaxL) in a per-wave list by
+    // ballot compaction, and every position of that own run walks the list.  The
+    // list keeps run order, so the strict > keeps the leftmost maximum.
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    uint2 *wl2 = (uint2 *)(rt - kRunListWords) + 64 * wv;    // per-wave candidate list (se, ext)
+    bool left = false;
+    for (uint32_t c0 = q0 + 64 * wv; c0 < npos; c0 += kMT) {
+        const uint32_t x = c0 + lane;
+        const bool need = x < npos && step[x - q0] == 0;
+        if (__ballot(need) == 0ull) continue;
+        const uint32_t xv = min(x, npos - 1);
+        const uint32_t cap = min(kMaxL, ilen - xv) - 1;
+        const uint32_t xlo = max(w0 + xv, kWin) - kWin - w0;
+        const uint32_t ko = run_rank(rbm, prc, xv) - 1;
+        const uint32_t kfirst = __shfl(ko, 0, 64), klast = __shfl(ko, 63, 64);
+        uint32_t res = 0;
+        bool lost = need && nruns > kRunTableCap;
+        for (uint32_t kr = kfirst; kr <= klast && nruns <= kRunTableCap; kr++) {
+            const bool mine = need && ko == kr;
+            const uint64_t in_run = __ballot(mine);
+            if (in_run == 0ull) continue;
+            const uint32_t own = rt[kr], cb = own >> 16;
+            const uint32_t e = rt[kr + 1] & 0xFFFFu;
+            const uint32_t xf = c0 + (uint32_t)__builtin_ctzll(in_run);     // first position of the run here
+            const uint32_t klo = run_rank(rbm, prc, max(w0 + xf, kWin) - kWin - w0) - 1;
+            if (kr - klo > kRunBudget) { lost = lost || mine; continue; }
+            const uint32_t r = e - xv;
+            const bool big = r > cap;
+            uint32_t best = 0;   // packed L << 13 | (8191 - j): max = longest, then leftmost
+            const uint32_t vb0 = rt[kr + 1];
+            for (uint32_t k0 = klo; k0 < kr; k0 += 64) {
+                const uint32_t kc = k0 + lane;
+                bool cand = false;
+                uint32_t se = 0, ext = 0;
+                if (kc < kr) {
+                    const uint32_t v = rt[kc], nv = rt[kc + 1];
+                    if ((v >> 16) == cb) {
+                        cand = true;
+                        se = (v & 0xFFFFu) | (nv << 16);
+                        // ext: equal (byte, length) runs extend it; the first run that
+                        // differs in length adds the shorter length and ends it.  The
+                        // query side meets the image end (sentinel) only past the cap.
+                        uint32_t ka = kc + 1, kb = kr + 1, va = nv, vb = vb0;
+                        while ((va >> 16) == (vb >> 16)) {
+                            const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
+                            const uint32_t la = (na & 0xFFFFu) - (va & 0xFFFFu), lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
+                            if (la != lb) { ext += min(la, lb); break; }
+                            ext += la;
+                            if (ext >= kMaxL) break;
+                            ka++; kb++; va = na; vb = nb;
+                        }
+                    }
+                }
+                const uint64_t cm = __ballot(cand);
+                if (cand) {
+                    const uint32_t slot = (uint32_t)__builtin_popcountll(cm & ((1ull << lane) - 1ull));
+                    wl2[slot] = make_uint2(se, ext);
+                }
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t n = (uint32_t)__builtin_popcountll(cm);
+                if (mine)
+                    for (uint32_t t = 0; t < n; t++) {   // branch-free candidate value
+                        const uint2 w = wl2[t];
+                        const uint32_t ep = w.x >> 16;
+                        const uint32_t sp = max(w.x & 0xFFFFu, xlo);
+                        const uint32_t A = ep - sp;
+                        const uint32_t Lr = min(r + w.y, cap);
+                        const bool ge = !big && A >= r;
+                        const uint32_t Lc = ge ? Lr : min(A, cap);
+                        const uint32_t j = (ge && w.y != 0 && r < cap) ? ep - r : sp;
+                        const uint32_t key = (Lc << 13) | (8191u - j);
+                        best = (ep > xlo && key > best) ? key : best;
+                    }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (mine) {
+                const uint32_t sp = max(own & 0xFFFFu, xlo);
+                if (sp < xv) best = max(best, ((big ? cap : r) << 13) | (8191u - sp));
+                const uint32_t bL = best >> 13, bj = 8191u - (best & 0x1FFFu);
+                res = bL >= kMinL ? m_pack(bL, xv - bj) : 0u;
+            }
+        }
+        if (mbx) {   // whole-tile mode: this wave writes the positions' mbits word and m row
+            const uint64_t mb = __ballot(need && !lost && res != 0), lb = __ballot(lost);
+            if (lane == 0) mbx[c0 >> 6] = mb | lb;
+            if (lost) mx[x] = kUnknown;
+            else if (mb && need) mx[x] = res;
+        } else if (need && !lost) {
+            mx[x] = res;
+        }
+        if (need && !lost) step[x - q0] = (uint16_t)(res ? m_len(res) + 1 : 1);
+        left = left || lost;
+    }
+    if (left) *s_unknown = 1;
+    __syncthreads();
+}
 
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
@@ -55,11 +199,12 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __shared__ uint32_t sdw[kTileBytes / 4 + 4];           // byte image of the window
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
     // search, [step (u16 x 4096) | parse scratch] after it
-    __shared__ uint32_t region[kRegionWords];
+    __shared__ __attribute__((aligned(16))) uint32_t region[kRegionWords];
     uint32_t *hw = region;                                  // packed u16 bucket counters, then starts
     uint16_t *h16 = (uint16_t *)region;
     uint16_t *ent = (uint16_t *)(region + kHeadWords);     // window entries, bucket-sorted
     __shared__ uint32_t s_unknown;
+    __shared__ uint32_t s_nruns;
     __shared__ uint32_t s_chg[2];
     __shared__ uint32_t s_red[3 * kWaves];   // cross-wave scan partials
 
@@ -95,14 +240,42 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             sdw[x] = v;
         }
     }
+    if (tid == 0) { s_unknown = 0; s_nruns = 0; s_chg[0] = 0; s_chg[1] = 0; }
+    __syncthreads();
+    const uint32_t npos = t1 - w0;
+    const uint32_t q0 = t0 - w0;
+    uint16_t *step = (uint16_t *)region;               // after the search: L + 1 per position, 0 = unknown
+
+    // ---- 1b. run count of the image: a tile of long runs (zeros, runs) skips the
+    // bucket search and takes every match from the run table (dense_phase) ----
+    {
+        // per dword: bytes differing from their predecessor (byte 0 of the image counts once)
+        uint32_t cnt = tid == 0 && nload > 0 ? 1u : 0u;
+        for (uint32_t w = tid; 4 * w < nload; w += kMT) {
+            const uint32_t v = sdw[w], pv = w ? sdw[w - 1] : v << 24;
+            uint32_t x = v ^ ((v << 8) | (pv >> 24));
+            x |= x >> 4; x |= x >> 2; x |= x >> 1;
+            uint32_t msk = x & 0x01010101u;
+            const uint32_t nb = nload - 4 * w;
+            if (nb < 4) msk &= (1u << (8 * nb)) - 1u;
+            cnt += (uint32_t)__builtin_popcount(msk);
+        }
+        cnt = wave_sum_u32(cnt);
+        if ((tid & 63) == 0) atomicAdd(&s_nruns, cnt);
+    }
+    __syncthreads();
+    const bool rmode = (s_nruns <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
+
+    if (rmode) {
+        for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
+        if (tid == 0) s_unknown = 1;
+        __syncthreads();
+    } else {
     for (uint32_t x = tid; x < kHeadWords; x += kMT) hw[x] = 0;
-    if (tid == 0) { s_unknown = 0; s_chg[0] = 0; s_chg[1] = 0; }
     __syncthreads();
 
     // ---- 2. counting sort of the window positions by bucket ----
     // 16-bit counters, two per dword (a bucket never exceeds 6144 entries)
-    const uint32_t npos = t1 - w0;
-    const uint32_t q0 = t0 - w0;
     const uint32_t ins_end = min(npos, blen >= 3 ? blen - 2 - w0 : 0);  // j + 3 <= blen
     constexpr uint32_t kIns = (kWinPos + kMT - 1) / kMT;               // 12 per lane
     uint32_t ins_hr[kIns];                                             // bucket << 16 | rank
@@ -228,6 +401,15 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         }
     }
     __syncthreads();   // the search region is dead from here on
+#pragma unroll
+    for (uint32_t r = 0; r < kQPL; r++) step[tid + kMT * r] = (uint16_t)(st_reg[r >> 1] >> (16 * (r & 1)));
+    __syncthreads();
+    }   // bucket search
+
+    // ---- 3b. dense windows: exact matches of the unknown positions over the run table ----
+    if (s_unknown != 0)
+        dense_phase(sdw, region, step, s_red, &s_unknown, m + bstart + w0,
+                    rmode ? mbits + (uint64_t)b * L.wpb + (w0 >> 6) : nullptr, q0, npos, nload, blen - w0, w0);
 
     uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
     uint32_t *ti = tinfo + 8ull * blockIdx.x;
@@ -239,13 +421,9 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
 
     // ---- 4. tile-local greedy parse ----
-    uint16_t *step = (uint16_t *)region;               // 8 KB
     uint32_t *Gs = region + kTile / 2;                 // kMT + 1 entries
     uint32_t *Xs = Gs + kMT + 1;
     uint32_t *Vs = Xs + kMT;
-#pragma unroll
-    for (uint32_t r = 0; r < kQPL; r++) step[tid + kMT * r] = (uint16_t)(st_reg[r >> 1] >> (16 * (r & 1)));
-    __syncthreads();
     const uint32_t s = t0 + tid * kSeg;
     const uint32_t se = min(s + kSeg, t1);
     uint32_t V = 0, X = s;
@@ -258,23 +436,39 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     Gs[tid + 1] = X;
     if (tid == 0) Gs[0] = t0;
     __syncthreads();
+    // Jacobi rounds.  A segment is active when its entry lies inside it; the next
+    // entry of segment k + 1 is the exit of the nearest active segment <= k (a
+    // block-wide running max of active indices), so a long token passes over any
+    // number of segments in one round.
     uint32_t T = 0;
+    uint32_t *Ys = Vs;   // exits of this round (Vs is free until the counts below)
     for (uint32_t r = 0;; r++) {
         const uint32_t e = Gs[tid];
         uint32_t ex;
+        bool act = false;
         if (s >= t1 || e >= se) {
             ex = e; T = 0;
         } else if ((V >> (e - s)) & 1u) {
-            ex = X; T = V & (~0u << (e - s));
+            act = true; ex = X; T = V & (~0u << (e - s));
         } else {
-            T = 0;
+            act = true; T = 0;
             uint32_t t = e;
             while (t < se && !((V >> (t - s)) & 1u)) { T |= 1u << (t - s); t += step[t - t0]; }
             if (t < se) { ex = X; T |= V & (~0u << (t - s)); }
             else ex = t;
         }
+        Ys[tid] = ex;
+        // nearest active segment <= tid: highest set bit of the wave's ballot at or
+        // below this lane, else the last active segment of an earlier wave
+        const uint64_t am = __ballot(act);
+        const uint32_t lane = tid & 63;
+        if (lane == 0) s_red[tid >> 6] = am ? (tid & ~63u) + 64 - (uint32_t)__clzll(am) : 0u;
         __syncthreads();
-        if (ex != Gs[tid + 1]) { Gs[tid + 1] = ex; s_chg[r & 1] = 1; }
+        const uint64_t le = am & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        uint32_t li = le ? (tid & ~63u) + 64 - (uint32_t)__clzll(le) : 0u;
+        for (int w = (int)(tid >> 6) - 1; w >= 0 && !li; w--) li = s_red[w];
+        const uint32_t ne = li ? Ys[li - 1] : Gs[tid + 1];
+        if (ne != Gs[tid + 1]) { Gs[tid + 1] = ne; s_chg[r & 1] = 1; }
         if (tid == 0) s_chg[(r + 1) & 1] = 0;
         __syncthreads();
         if (!s_chg[r & 1]) break;
@@ -327,7 +521,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                   uint32_t *tinfo, hipStream_t st) {
-    // FCX_MATCH_DBG (experiments only, output invalid when set): bit0 skip searches, bit1 skip long extension
+    // FCX_MATCH_DBG (experiments only): bit0 skip searches, bit1 skip long extension (both: output invalid),
+    // bit2 never / bit3 always take the whole-tile run mode (output stays exact)
     static const uint32_t dbg = getenv("FCX_MATCH_DBG") ? (uint32_t)atoi(getenv("FCX_MATCH_DBG")) : 0u;
     const uint32_t grid = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, dbg);

@@ -317,8 +317,28 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         lazy_tiles += lazy ? 1 : 0;
         mbL[lane] = lane < nw ? mb[lane] : 0ull;   // one mbits word per lane (64 words per tile)
         __syncthreads();
-        for (uint32_t x = lane; x < t1 - t0; x += 64)   // m only where the position's mbits bit is set
-            mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? mt[x] : 0u;
+        const uint32_t nt = t1 - t0;
+        if ((((uintptr_t)mt) & 15) == 0) {   // 16 independent 16-B loads per lane, then masked LDS stores
+            uint4 v[kTile / 256];
+#pragma unroll
+            for (uint32_t q = 0; q < kTile / 256; q++) {
+                const uint32_t x = 4 * (lane + 64 * q);
+                v[q] = x + 4 <= nt ? ((const uint4 *)mt)[lane + 64 * q] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kTile / 256; q++) {
+                const uint32_t x = 4 * (lane + 64 * q);
+                if (x >= nt) continue;
+                const uint32_t mbw = (uint32_t)(mbL[x >> 6] >> (x & 63)) & 0xFu;
+                const uint32_t vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++)
+                    if (x + u < nt) mL[x + u] = ((mbw >> u) & 1u) ? (x + 4 <= nt ? vv[u] : mt[x + u]) : 0u;
+            }
+        } else {
+            for (uint32_t x = lane; x < nt; x += 64)   // m only where the position's mbits bit is set
+                mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? mt[x] : 0u;
+        }
         for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
         __syncthreads();
         if (e > t0) bm_apply(bmL, 0xFFFFFFFFu, 0, e - t0);
