@@ -36,7 +36,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HL_DIGEST = {  # reference output digests for the N=1 shards
     ("rand", 4, 1 << 30, 1 << 20): ("ee962534628bf6b2f79c51a44a65ac0845945e2fe9225e5be8f99f288912a69d", 1091294206),
     ("text", 3, 1 << 30, 1 << 20): ("132a36b9d2592f8c37a82b51f545ddb67acec53fa1a31b7f1f6a04617a01a3d1", 624801500),
+    ("text", 3, 1 << 30, 1 << 18): ("20219e60c2e9aef6659801fbfc53c6873ec811686eedcb45c0896fc5547d63d0", 630008807),
+    ("zeros", 0, 1 << 30, 1 << 20): ("533fd45fbaa861a6060e9a5beac177cc0b64db691fc602a1e0e1e188afa5f912", 7521290),
+    ("runs", 5, 1 << 30, 1 << 20): ("4fced94fd4725ba3b1031dec67d63e1295b95ae08cc1cf0e34c84769f5313d26", 42548682),
 }
+# extra legs measured after the main one: name -> (kind, seed, block bytes); BASELINE configs 3 and 5
+LEGS = {"text": ("text", 3, 1 << 20), "c3": ("text", 3, 1 << 18), "zeros": ("zeros", 0, 1 << 20),
+        "runs": ("runs", 5, 1 << 20)}
 
 
 def log(*a):
@@ -62,20 +68,21 @@ def make_shard(kind, seed, rank, n):
     return host
 
 
-def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages):
+def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages, block=None):
     import torch
 
     import my_compress_amd as mc
 
     n = args.mib << 20
+    block = block or args.block
     t = time.time()
     host = make_shard(kind, seed, rank, n)
     gen_s = time.time() - t
     d_in = host.to(dev)
     del host
-    cap = mc.shard_bound(n, args.block)
+    cap = mc.shard_bound(n, block)
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
-    ctx = mc.Context(dev.index, args.block, n)
+    ctx = mc.Context(dev.index, block, n)
     stream = torch.cuda.current_stream(dev)
     sid = stream.cuda_stream
     out_len = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid)  # validates the call
@@ -105,7 +112,7 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages):
         dt = float(tt.item())
     out_len = ctx.read_out_len()   # segment size of the timed steps (device word)
     res = {
-        "kind": kind, "bytes_per_gpu": n, "out_bytes": out_len, "ratio": out_len / n,
+        "kind": kind, "block_bytes": block, "bytes_per_gpu": n, "out_bytes": out_len, "ratio": out_len / n,
         "seconds": dt, "ms_per_step": dt / args.steps * 1e3,
         "value": world * n * args.steps / dt / 1e6, "gen_s": gen_s,
         "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
@@ -113,11 +120,11 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages):
     stats = ctx.stats()
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
-    key = (kind, seed, n, args.block)
+    key = (kind, seed, n, block)
     if rank == 0 and world == 1 and key in HL_DIGEST and not args.no_verify:
         import my_compress_amd as mc2
 
-        h = hashlib.sha256(mc2.write_header(n, (n + args.block - 1) // args.block))
+        h = hashlib.sha256(mc2.write_header(n, (n + block - 1) // block))
         h.update(memoryview(d_out[:out_len].cpu().numpy()))
         want_sha, want_bytes = HL_DIGEST[key]
         res["bit_exact_vs_reference"] = h.hexdigest() == want_sha and out_len + 10 == want_bytes
@@ -159,9 +166,22 @@ def allgather_concat(d_out, seg_len, world, dev, dist):
             "GBps_per_rank_recv": (total - seg_len) / dt / 1e9}
 
 
-def cpu_baseline(kind, seed, block, threads=16, nblocks=32):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(kind, seed, block, threads=16, nblocks=32, nblocks_1t=4):
     """the reference's block encoder (oracle/_ref, compiled from /root/reference) on
-    the first nblocks blocks of the same shard, `threads` host threads"""
+    the first nblocks blocks of the same shard, `threads` host threads (the box's
+    CPU share), plus the first nblocks_1t blocks on one thread (the reference is
+    single-threaded)"""
     import oracle
 
     R = oracle.ref()
@@ -190,6 +210,14 @@ def cpu_baseline(kind, seed, block, threads=16, nblocks=32):
 
     if R is not None:
         R.ref_set_quiet(1)
+    t1 = time.perf_counter()
+    ob1 = ctypes.create_string_buffer(2 * block + 4096)
+    for i in range(min(nblocks_1t, len(blocks))):
+        if R is not None:
+            R.ref_compress_block(blocks[i], len(blocks[i]), ob1)
+        else:
+            oracle.orc().orc_compress_block(blocks[i], len(blocks[i]), ob1, oracle.FINDER_SUNDAY)
+    one = min(nblocks_1t, len(blocks)) * block / (time.perf_counter() - t1) / 1e6
     t0 = time.perf_counter()
     ths = [threading.Thread(target=worker) for _ in range(threads)]
     for t in ths:
@@ -202,7 +230,8 @@ def cpu_baseline(kind, seed, block, threads=16, nblocks=32):
     return {"value": n / dt / 1e6, "unit": "MB/s", "cores": threads, "kind": kind_used,
             "sample": f"first {nblocks} x {block // 1024} KiB blocks of the {kind} shard, {threads} threads "
                       f"({'reference my_compress_file_lz77 compiled in place' if R is not None else 'oracle port'})",
-            "seconds": dt}
+            "seconds": dt, "one_thread_MBps": one, "one_thread_sample": f"first {nblocks_1t} blocks, 1 thread",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count()}
 
 
 def load_pmc(path):
@@ -220,7 +249,9 @@ def main():
     ap.add_argument("--kind", default="rand", choices=["rand", "text", "runs", "zeros"])
     ap.add_argument("--mib", type=int, default=1024, help="MiB per GPU")
     ap.add_argument("--block", type=int, default=1 << 20)
-    ap.add_argument("--no-text", action="store_true", help="skip the text leg")
+    ap.add_argument("--no-text", action="store_true", help="skip every extra leg")
+    ap.add_argument("--legs", default="text,c3,zeros,runs",
+                    help="extra legs after the main one (comma list of " + ",".join(LEGS) + ")")
     ap.add_argument("--concat", default="allgather", choices=["allgather", "none"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -247,9 +278,12 @@ def main():
         dist = dist_
     seeds = {"rand": 4, "text": 3, "runs": 5, "zeros": 0}
     main_res, concat = run_leg(args.kind, seeds[args.kind], args, rank, world, dev, dist, True)
-    text_res = None
-    if not args.no_text and args.kind != "text":
-        text_res, _ = run_leg("text", 3, args, rank, world, dev, dist, True)
+    legs = {}
+    for name in ([] if args.no_text else [x for x in args.legs.split(",") if x]):
+        kind, seed, block = LEGS[name]
+        if kind == args.kind and block == args.block:
+            continue
+        legs[name], _ = run_leg(kind, seed, args, rank, world, dev, dist, True, block=block)
 
     if rank == 0:
         stages = {k: v for k, v in main_res["stages_ms"].items() if k != "memset"}
@@ -276,7 +310,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: glibc rand()%256 seed 4, rank r = bytes [r*shard, (r+1)*shard) of one stream "
-                    "(SURVEY.md §8(d)); text leg: SURVEY enwik-style generator, seed 3+rank",
+                    "(SURVEY.md §8(d)); extra legs: text = enwik-style generator seed 3+rank at 1 MiB (HL-text) "
+                    "and 256 KiB blocks (c3), zeros, runs seed 5+rank (BASELINE config 5)",
             "config": {"workload": f"{args.kind} {args.mib} MiB per GPU, {args.block // 1024} KiB blocks "
                                    f"(BASELINE config 4 sharding; N=1 = HL-{args.kind})",
                        "kind": args.kind, "bytes_per_gpu": n, "block_bytes": args.block,
@@ -289,9 +324,9 @@ def main():
             "lazy_evals": main_res["lazy_evals"],
             "concat": concat,
         }
-        if text_res:
-            line["text"] = {k: text_res[k] for k in ["value", "ms_per_step", "ratio", "stages_ms", "lazy_evals"]}
-            line["text"]["bit_exact_vs_reference"] = text_res.get("bit_exact_vs_reference")
+        for name, lr in legs.items():
+            line[name] = {k: lr[k] for k in ["value", "ms_per_step", "ratio", "block_bytes", "stages_ms", "lazy_evals"]}
+            line[name]["bit_exact_vs_reference"] = lr.get("bit_exact_vs_reference")
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

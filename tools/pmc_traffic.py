@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
 """Summarise tools/pmc_traffic.sh output into profiles/pmc_<tag>.json (+ pmc_latest.json).
+Keys are "<leg>:<stage>" (legs rand, text, c3 = text at 256 KiB blocks, zeros, runs).
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch (summed over XCDs).  On gfx950 FETCH_SIZE
 tallies 128-B requests at 64 B (MI355X_MICROARCH.md §HBM), so read bytes = 2 x FETCH_SIZE
@@ -15,7 +16,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "latest"
 out = {}
-for kind in ["rand", "text"]:
+names = sorted({os.path.basename(d).split("_")[1] for d in glob.glob(os.path.join(ROOT, "gpurun_out/traffic_*_FETCH_SIZE"))})
+for kind in names:
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for ctr in ["FETCH_SIZE", "WRITE_SIZE"]:
         for f in glob.glob(os.path.join(ROOT, f"gpurun_out/traffic_{kind}_{ctr}/run_counter_collection.csv")):
