@@ -128,6 +128,8 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages, block=None
         h.update(memoryview(d_out[:out_len].cpu().numpy()))
         want_sha, want_bytes = HL_DIGEST[key]
         res["bit_exact_vs_reference"] = h.hexdigest() == want_sha and out_len + 10 == want_bytes
+    if not args.no_decode:
+        res["decode"] = decode_leg(d_out, out_len, n, block, d_in, args, dev, dist, world)
     concat = None
     if dist and world > 1 and args.concat == "allgather":
         concat = allgather_concat(d_out, out_len, world, dev, dist)
@@ -135,6 +137,50 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages, block=None
     del d_in, d_out
     torch.cuda.empty_cache()
     return res, concat
+
+
+def decode_leg(d_rec, rec_len, n, block, d_in, args, dev, dist, world):
+    """GPU decoder on the leg's own records: K timed
+    fcx_decompress_shard calls (device records -> device bytes), max over ranks,
+    then a byte compare with the input"""
+    import torch
+
+    import my_compress_amd as mc
+
+    nblocks = (n + block - 1) // block
+    d_back = torch.empty(n, dtype=torch.uint8, device=dev)
+    dctx = mc.DContext(dev.index)
+    sid = torch.cuda.current_stream(dev).cuda_stream
+    try:
+        for _ in range(max(1, args.warmup)):
+            dctx.decompress_shard(d_rec.data_ptr(), rec_len, nblocks, d_back.data_ptr(), n, sid)
+        dctx.set_profiling(True)
+        stage_sum = {}
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            dctx.decompress_shard(d_rec.data_ptr(), rec_len, nblocks, d_back.data_ptr(), n, sid)
+            for name, ms in dctx.stage_times():
+                stage_sum[name] = stage_sum.get(name, 0.0) + ms
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist:
+            tt = torch.tensor([dt], dtype=torch.float64)
+            if dist.get_backend() != "gloo":
+                tt = tt.to(dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        ok = bool(torch.equal(d_back, d_in))
+    finally:
+        dctx.close()
+    del d_back
+    return {"value": world * n * args.steps / dt / 1e6, "unit": "MB/s (decoded bytes)",
+            "ms_per_step": dt / args.steps * 1e3, "round_trip_exact": ok,
+            "stages_ms": {k: v / args.steps for k, v in stage_sum.items()}}
 
 
 def allgather_concat(d_out, seg_len, world, dev, dist):
@@ -255,6 +301,7 @@ def main():
     ap.add_argument("--concat", default="allgather", choices=["allgather", "none"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decode", action="store_true", help="skip the GPU decoder timing")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     args = ap.parse_args()
@@ -323,9 +370,12 @@ def main():
             "stages_ms": main_res["stages_ms"],
             "lazy_evals": main_res["lazy_evals"],
             "concat": concat,
+            "decode": main_res.get("decode"),
         }
         for name, lr in legs.items():
             line[name] = {k: lr[k] for k in ["value", "ms_per_step", "ratio", "block_bytes", "stages_ms", "lazy_evals"]}
+            if "decode" in lr:
+                line[name]["decode"] = lr["decode"]
             line[name]["bit_exact_vs_reference"] = lr.get("bit_exact_vs_reference")
         print(json.dumps(line), flush=True)
     if dist:

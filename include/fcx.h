@@ -12,6 +12,10 @@
  *   fcx_compress_shard    <- main()'s per-block compress loop                      :4090-4122
  *                            (batched: every block of a device-resident shard in one
  *                             launch sequence, emitting [u32 len][payload]...)
+ *   fcx_decompress_shard  <- main()'s per-block decompress loop, my_decompress_file_lz77
+ *                            per record                                            :4160-4204, :2255
+ *                            (GPU decoder: every record of a device-resident run)
+ *   fcx_decompress_host   <- the whole decompress mode of main() on host buffers  :4137-4204
  *
  * Conventions: plain pointers and sizes, no exceptions cross the ABI, every
  * function returns FCX_OK (0) or a negative FCX_ERR_* code unless stated; the
@@ -106,6 +110,33 @@ int fcx_ctx_stage(fcx_ctx *ctx, int i, const char **name, float *ms);
  * tokens, matches, lazily evaluated positions, lazy tiles, total tiles */
 int fcx_ctx_stats(fcx_ctx *ctx, uint64_t *tokens, uint64_t *matches, uint64_t *lazy_evals,
                   uint64_t *lazy_tiles, uint64_t *tiles);
+
+/* ---- GPU decoder ------------------------------------------------------------ */
+
+typedef struct fcx_dctx fcx_dctx;
+
+/* Decoder context on HIP device `device`; scratch grows on demand. */
+int fcx_dctx_create(fcx_dctx **ctx, int device);
+void fcx_dctx_destroy(fcx_dctx *ctx);
+
+/* Decodes `nblocks` consecutive block records ([u32 len][payload]..., an FCX7
+ * file without its 10-byte header) of in_len device-resident bytes at d_in into
+ * d_out (device, capacity cap), blocks back to back in order.  The bytes equal
+ * the reference decoder's (my_decompress_file_lz77 :2255), including its
+ * single-symbol sub-stream and early-stop behaviour.  Synchronises `stream` (a
+ * hipStream_t; NULL = default) once after the header pass (to size scratch) and
+ * once at the end; stores the decoded byte count in *out_len.  FCX_ERR_FORMAT
+ * for malformed input, FCX_ERR_CAPACITY if cap is too small. */
+int fcx_decompress_shard(fcx_dctx *ctx, const uint8_t *d_in, uint64_t in_len, uint32_t nblocks, uint8_t *d_out,
+                         uint64_t cap, uint64_t *out_len, void *stream);
+/* Host-to-host: a whole FCX7 file (header included) into `out`, in groups of up
+ * to 1024 records per device call. */
+int fcx_decompress_host(fcx_dctx *ctx, const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t cap,
+                        uint64_t *out_len);
+/* per-stage hipEvent timing of subsequent fcx_decompress_shard calls */
+int fcx_dctx_set_profiling(fcx_dctx *ctx, int enable);
+int fcx_dctx_stage_count(fcx_dctx *ctx);
+int fcx_dctx_stage(fcx_dctx *ctx, int i, const char **name, float *ms);
 
 const char *fcx_last_error(void);
 const char *fcx_version(void);

@@ -71,6 +71,18 @@ def lib():
     L.fcx_ctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                 ctypes.POINTER(ctypes.c_float)]
     L.fcx_ctx_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
+    L.fcx_dctx_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
+    L.fcx_dctx_destroy.argtypes = [ctypes.c_void_p]
+    L.fcx_dctx_destroy.restype = None
+    L.fcx_decompress_shard.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.c_void_p]
+    L.fcx_decompress_host.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64)]
+    L.fcx_dctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.fcx_dctx_stage_count.argtypes = [ctypes.c_void_p]
+    L.fcx_dctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                 ctypes.POINTER(ctypes.c_float)]
     L.fcx_last_error.restype = ctypes.c_char_p
     L.fcx_version.restype = ctypes.c_char_p
     _lib = L
@@ -152,6 +164,67 @@ class Context:
         vals = [ctypes.c_uint64() for _ in range(5)]
         _check(lib().fcx_ctx_stats(self._h, *[ctypes.byref(v) for v in vals]), "fcx_ctx_stats")
         return dict(zip(["tokens", "matches", "lazy_evals", "lazy_tiles", "tiles"], [v.value for v in vals]))
+
+
+class DContext:
+    """fcx_dctx: the GPU decoder (my_decompress_file_lz77 :2255 for whole runs of block records)."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().fcx_dctx_create(ctypes.byref(self._h), device), "fcx_dctx_create")
+
+    def close(self):
+        if self._h:
+            lib().fcx_dctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decompress_shard(self, d_in: int, in_len: int, nblocks: int, d_out: int, cap: int, stream: int = 0) -> int:
+        """device records in, decoded bytes at d_out; returns the decoded byte count"""
+        out = ctypes.c_uint64(0)
+        _check(lib().fcx_decompress_shard(self._h, ctypes.c_void_p(d_in), in_len, nblocks, ctypes.c_void_p(d_out),
+                                          cap, ctypes.byref(out), ctypes.c_void_p(stream)), "fcx_decompress_shard")
+        return out.value
+
+    def decompress_host(self, blob: bytes, cap: int = None) -> bytes:
+        """a whole FCX7 file -> the decoded bytes, on the GPU"""
+        if cap is None:
+            cap = max(16, struct.unpack_from("<I", blob, 4)[0] if len(blob) >= HEADER_BYTES else 0)
+        out = ctypes.create_string_buffer(cap)
+        got = ctypes.c_uint64(0)
+        _check(lib().fcx_decompress_host(self._h, blob, len(blob), out, cap, ctypes.byref(got)),
+               "fcx_decompress_host")
+        return out.raw[:got.value]
+
+    def set_profiling(self, on: bool = True):
+        _check(lib().fcx_dctx_set_profiling(self._h, 1 if on else 0), "fcx_dctx_set_profiling")
+
+    def stage_times(self):
+        res = []
+        for i in range(lib().fcx_dctx_stage_count(self._h)):
+            name = ctypes.c_char_p()
+            ms = ctypes.c_float()
+            _check(lib().fcx_dctx_stage(self._h, i, ctypes.byref(name), ctypes.byref(ms)), "fcx_dctx_stage")
+            res.append((name.value.decode(), ms.value))
+        return res
+
+
+def decompress_gpu(blob: bytes, cap: int = None, device: int = 0, ctx: "DContext" = None) -> bytes:
+    """whole FCX7 file -> bytes with the GPU decoder (cap defaults to the header's total,
+    which wraps mod 2^32: pass cap for larger files)"""
+    own = ctx is None
+    if own:
+        ctx = DContext(device)
+    try:
+        return ctx.decompress_host(blob, cap)
+    finally:
+        if own:
+            ctx.close()
 
 
 def my_compress_file_lz77(block: bytes) -> bytes:

@@ -73,6 +73,10 @@ Layout make_layout(uint64_t n, uint32_t B) {
 }
 }  // namespace
 
+namespace fcx {
+void set_last_error(const std::string &m) { g_err = m; }
+}  // namespace fcx
+
 struct fcx_ctx {
     int device = 0;
     uint32_t B = 0;
