@@ -93,11 +93,28 @@ const uint64_t *fcx_ctx_device_out_len(fcx_ctx *ctx);
 /* waits for the device and reads that length (and the device error bits) */
 int fcx_ctx_read_out_len(fcx_ctx *ctx, uint64_t *out_len);
 
-/* Host-to-host convenience for the CLI: compresses host memory in shards of up
- * to the context's shard size (H2D, device pipeline, D2H) and writes the same
+/* Host-to-host convenience: compresses host memory in shards of the context's
+ * shard size through the pipelined stream path below and writes the same
  * [u32 len][payload]... stream to host `out` (capacity cap). */
 int fcx_compress_host(fcx_ctx *ctx, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap,
                       uint64_t *out_len);
+/* device, block size and shard capacity of a context (any pointer may be NULL) */
+int fcx_ctx_info(fcx_ctx *ctx, int *device, uint32_t *block_bytes, uint64_t *shard_bytes);
+
+/* ---- pipelined host I/O (main()'s read / code / write loop, :4073-4204) ----- */
+
+/* read: fill up to cap bytes, return the count (0 = end of input) or < 0 on error;
+ * write: consume n bytes, return 0 or < 0 on error */
+typedef int64_t (*fcx_read_fn)(void *user, uint8_t *buf, uint64_t cap);
+typedef int (*fcx_write_fn)(void *user, const uint8_t *buf, uint64_t n);
+
+/* Streams input through the GPU in shards of shard_bytes (rounded down to whole
+ * blocks): two pinned/device slots, H2D / compute / D2H on separate streams, the
+ * next shard read and the previous shard's records written while the GPU
+ * compresses.  Emits the [u32 len][payload]... records (no file header; the
+ * caller writes it from *total_in and *nblocks). */
+int fcx_compress_stream(fcx_ctx *ctx, fcx_read_fn read, fcx_write_fn write, void *user, uint64_t shard_bytes,
+                        uint64_t *total_in, uint64_t *total_out, uint64_t *nblocks);
 
 /* ---- introspection ---------------------------------------------------------- */
 
@@ -129,10 +146,16 @@ void fcx_dctx_destroy(fcx_dctx *ctx);
  * for malformed input, FCX_ERR_CAPACITY if cap is too small. */
 int fcx_decompress_shard(fcx_dctx *ctx, const uint8_t *d_in, uint64_t in_len, uint32_t nblocks, uint8_t *d_out,
                          uint64_t cap, uint64_t *out_len, void *stream);
-/* Host-to-host: a whole FCX7 file (header included) into `out`, in groups of up
- * to 1024 records per device call. */
+/* Host-to-host: a whole FCX7 file (header included) into `out` (capacity cap),
+ * through fcx_decompress_stream. */
 int fcx_decompress_host(fcx_dctx *ctx, const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t cap,
                         uint64_t *out_len);
+/* Streams an FCX7 file (header first) through the GPU decoder in groups of up
+ * to 256 whole records; max_in (0 = unknown) bounds the staging buffers.
+ * Reports the header's total (mod 2^32), the decoded bytes and the records. */
+int fcx_decompress_stream(fcx_dctx *ctx, fcx_read_fn read, fcx_write_fn write, void *user, uint64_t max_in,
+                          uint32_t *hdr_total, uint64_t *total_out, uint64_t *nblocks);
+int fcx_dctx_device(fcx_dctx *ctx, int *device);
 /* per-stage hipEvent timing of subsequent fcx_decompress_shard calls */
 int fcx_dctx_set_profiling(fcx_dctx *ctx, int enable);
 int fcx_dctx_stage_count(fcx_dctx *ctx);

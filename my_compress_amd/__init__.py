@@ -71,6 +71,12 @@ def lib():
     L.fcx_ctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                 ctypes.POINTER(ctypes.c_float)]
     L.fcx_ctx_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
+    L.fcx_compress_stream.argtypes = [ctypes.c_void_p, READ_FN, WRITE_FN, ctypes.c_void_p, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64)]
+    L.fcx_decompress_stream.argtypes = [ctypes.c_void_p, READ_FN, WRITE_FN, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_dctx_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
     L.fcx_dctx_destroy.argtypes = [ctypes.c_void_p]
     L.fcx_dctx_destroy.restype = None
@@ -87,6 +93,24 @@ def lib():
     L.fcx_version.restype = ctypes.c_char_p
     _lib = L
     return L
+
+
+# fcx_read_fn / fcx_write_fn (include/fcx.h)
+READ_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint64)
+WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint64)
+
+
+def _stream_fns(src, sink):
+    """ctypes callbacks over a binary reader (.readinto) and writer (.write)"""
+    def rd(_u, buf, cap):
+        mv = (ctypes.c_uint8 * cap).from_address(ctypes.addressof(buf.contents))
+        return src.readinto(memoryview(mv).cast("B"))
+
+    def wr(_u, buf, n):
+        sink.write(ctypes.string_at(buf, n))
+        return 0
+
+    return READ_FN(rd), WRITE_FN(wr)
 
 
 def _check(rc, what):
@@ -147,6 +171,15 @@ class Context:
         _check(lib().fcx_compress_host(self._h, data, len(data), out, cap, ctypes.byref(got)), "fcx_compress_host")
         return out.raw[:got.value]
 
+    def compress_stream(self, src, sink, shard_bytes: int):
+        """pipelined stream path: records of src (binary reader) to sink (binary writer);
+        returns (total_in, total_out, nblocks)"""
+        rd, wr = _stream_fns(src, sink)
+        vals = [ctypes.c_uint64() for _ in range(3)]
+        _check(lib().fcx_compress_stream(self._h, rd, wr, None, shard_bytes, *[ctypes.byref(v) for v in vals]),
+               "fcx_compress_stream")
+        return tuple(v.value for v in vals)
+
     def set_profiling(self, on: bool = True):
         _check(lib().fcx_ctx_set_profiling(self._h, 1 if on else 0), "fcx_ctx_set_profiling")
 
@@ -200,6 +233,16 @@ class DContext:
         _check(lib().fcx_decompress_host(self._h, blob, len(blob), out, cap, ctypes.byref(got)),
                "fcx_decompress_host")
         return out.raw[:got.value]
+
+    def decompress_stream(self, src, sink):
+        """FCX7 file from src (binary reader) to sink through the GPU decoder;
+        returns (header total, decoded bytes, records)"""
+        rd, wr = _stream_fns(src, sink)
+        t = ctypes.c_uint32()
+        o, n = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().fcx_decompress_stream(self._h, rd, wr, None, 0, ctypes.byref(t), ctypes.byref(o), ctypes.byref(n)),
+               "fcx_decompress_stream")
+        return t.value, o.value, n.value
 
     def set_profiling(self, on: bool = True):
         _check(lib().fcx_dctx_set_profiling(self._h, 1 if on else 0), "fcx_dctx_set_profiling")

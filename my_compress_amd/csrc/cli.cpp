@@ -5,8 +5,11 @@
 //   my_compress -i IN [-o OUT]             decompress
 //
 // Same flags, default output "./out" (4040-4042) and byte stream as the
-// reference.  Superset: -b/--block BYTES (<= 1 MiB; the reference fixes 1 MiB,
-// BLOCK_BYTES :113) and -d/--device N.  `-c lz78` (the LZ78 codec) is outside
+// reference.  Both directions stream through the GPU (fcx_compress_stream /
+// fcx_decompress_stream: file reads and writes overlap the device work); without
+// a HIP device, compress fails and decompress uses the host decoder.  Superset:
+// -b/--block BYTES (<= 1 MiB; the reference fixes 1 MiB, BLOCK_BYTES :113) and
+// -d/--device N.  `-c lz78` (the LZ78 codec) is outside
 // this build's scope and is rejected.
 #include <getopt.h>
 
@@ -26,35 +29,40 @@ static int usage() {
     return -1;
 }
 
+static int64_t file_read(void *u, uint8_t *buf, uint64_t cap) {
+    FILE *f = (FILE *)u;
+    const size_t n = fread(buf, 1, (size_t)cap, f);
+    return ferror(f) ? -1 : (int64_t)n;
+}
+
+struct Files {
+    FILE *in, *out;
+};
+static int64_t files_read(void *u, uint8_t *buf, uint64_t cap) { return file_read(((Files *)u)->in, buf, cap); }
+static int files_write(void *u, const uint8_t *buf, uint64_t n) {
+    return fwrite(buf, 1, (size_t)n, ((Files *)u)->out) == n ? 0 : -1;
+}
+
 static int do_compress(FILE *fin, FILE *fout, uint32_t block, int device) {
-    const uint64_t shard = 256ull << 20;  // host staging granule (multiple of any block size <= 1 MiB)
-    const uint64_t shard_blocks = shard / block;
-    const uint64_t shard_bytes = shard_blocks * block;
+    // 256 MiB shards through the pipelined stream path: the next shard is read and the
+    // previous one written while the GPU compresses (main()'s loop, 4073-4136)
+    const uint64_t shard = (256ull << 20) / block * block;
     fcx_ctx *ctx = nullptr;
-    if (fcx_ctx_create(&ctx, device, block, shard_bytes)) {
+    if (fcx_ctx_create(&ctx, device, block, shard)) {
         fprintf(stderr, "fcx: %s\n", fcx_last_error());
         return -1;
     }
     uint8_t hdr[FCX_HEADER_BYTES];
     fcx_write_header(hdr, 0, 0);  // placeholder, rewritten at the end (4079-4086, 4128-4129)
     fwrite(hdr, 1, sizeof(hdr), fout);
-    std::vector<uint8_t> in(shard_bytes), out(fcx_shard_bound(shard_bytes, block));
     uint64_t total_in = 0, total_out = 0, nblocks = 0;
+    Files io{fin, fout};
     auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-        const size_t got = fread(in.data(), 1, shard_bytes, fin);
-        if (got == 0) break;
-        uint64_t olen = 0;
-        if (fcx_compress_host(ctx, in.data(), got, out.data(), out.size(), &olen)) {
-            fprintf(stderr, "fcx: %s\n", fcx_last_error());
-            fcx_ctx_destroy(ctx);
-            return -1;
-        }
-        fwrite(out.data(), 1, olen, fout);
-        total_in += got;
-        total_out += olen;
-        nblocks += (got + block - 1) / block;
-        if (got < shard_bytes) break;
+    const int r = fcx_compress_stream(ctx, files_read, files_write, &io, shard, &total_in, &total_out, &nblocks);
+    if (r) {
+        fprintf(stderr, "fcx: %s\n", fcx_last_error());
+        fcx_ctx_destroy(ctx);
+        return -1;
     }
     fcx_write_header(hdr, total_in, nblocks);
     fseek(fout, 0, SEEK_SET);
@@ -70,7 +78,35 @@ static int do_compress(FILE *fin, FILE *fout, uint32_t block, int device) {
     return 0;
 }
 
-static int do_decompress(FILE *fin, FILE *fout) {
+// the reference compares sizes only (4198-4201)
+static int report(uint64_t got_total, uint32_t total) {
+    const bool ok = (uint32_t)got_total == total;
+    printf("All block decompress total bytes = %llu, Compress Before bytes = %u [%s]\n",
+           (unsigned long long)got_total, total, ok ? "SUCCESS" : "FAIL");
+    return ok ? 0 : 1;
+}
+
+// host decoder, used when no HIP device is present
+static int decompress_host(FILE *fin, FILE *fout, uint32_t total, uint16_t nblocks) {
+    std::vector<uint8_t> payload, plain(FCX_MAX_BLOCK_BYTES + 8);
+    uint64_t got_total = 0;
+    for (uint32_t b = 0; b < nblocks; b++) {
+        uint32_t sz = 0;
+        if (fread(&sz, 4, 1, fin) != 1) return -1;
+        payload.resize(sz);
+        if (fread(payload.data(), 1, sz, fin) != sz) return -1;
+        int64_t n = fcx_decompress_block(payload.data(), sz, plain.data(), plain.size());
+        if (n < 0) {
+            fprintf(stderr, "block %u: %s\n", b + 1, n == FCX_ERR_FORMAT ? "malformed" : "decode error");
+            return -1;
+        }
+        fwrite(plain.data(), 1, (size_t)n, fout);
+        got_total += (uint64_t)n;
+    }
+    return report(got_total, total);
+}
+
+static int do_decompress(FILE *fin, FILE *fout, int device) {
     uint8_t hdr[FCX_HEADER_BYTES];
     if (fread(hdr, 1, sizeof(hdr), fin) != sizeof(hdr)) {
         fprintf(stderr, "Read file head infomation error!!!\n");
@@ -87,26 +123,23 @@ static int do_decompress(FILE *fin, FILE *fout) {
         fprintf(stderr, "LZ78 streams are outside this build's scope\n");
         return -1;
     }
-    std::vector<uint8_t> payload, plain(FCX_MAX_BLOCK_BYTES + 8);
-    uint64_t got_total = 0;
-    for (uint32_t b = 0; b < nblocks; b++) {
-        uint32_t sz = 0;
-        if (fread(&sz, 4, 1, fin) != 1) return -1;
-        payload.resize(sz);
-        if (fread(payload.data(), 1, sz, fin) != sz) return -1;
-        int64_t n = fcx_decompress_block(payload.data(), sz, plain.data(), plain.size());
-        if (n < 0) {
-            fprintf(stderr, "block %u: %s\n", b + 1, n == FCX_ERR_FORMAT ? "malformed" : "decode error");
-            return -1;
-        }
-        fwrite(plain.data(), 1, (size_t)n, fout);
-        got_total += (uint64_t)n;
+    fcx_dctx *d = nullptr;
+    if (fcx_dctx_create(&d, device) != FCX_OK) {
+        fprintf(stderr, "fcx: %s; decoding on the host\n", fcx_last_error());
+        return decompress_host(fin, fout, total, nblocks);
     }
-    // the reference compares sizes only (4198-4201)
-    const bool ok = (uint32_t)got_total == total;
-    printf("All block decompress total bytes = %llu, Compress Before bytes = %u [%s]\n",
-           (unsigned long long)got_total, total, ok ? "SUCCESS" : "FAIL");
-    return ok ? 0 : 1;
+    // GPU decoder over whole records (the stream path re-reads the header)
+    rewind(fin);
+    Files io{fin, fout};
+    uint64_t got_total = 0, nrec = 0;
+    uint32_t htotal = 0;
+    const int r = fcx_decompress_stream(d, files_read, files_write, &io, 0, &htotal, &got_total, &nrec);
+    fcx_dctx_destroy(d);
+    if (r) {
+        fprintf(stderr, "fcx: %s\n", fcx_last_error());
+        return -1;
+    }
+    return report(got_total, total);
 }
 
 int main(int argc, char **argv) {
@@ -147,7 +180,7 @@ int main(int argc, char **argv) {
     if (!fin) { printf("open: %s Fail!!\n", file_in.c_str()); return -1; }
     FILE *fout = fopen(file_out.c_str(), "wb");
     if (!fout) { printf("open: %s Fail!!\n", file_out.c_str()); fclose(fin); return -1; }
-    const int r = compress ? do_compress(fin, fout, block, device) : do_decompress(fin, fout);
+    const int r = compress ? do_compress(fin, fout, block, device) : do_decompress(fin, fout, device);
     fclose(fin);
     fclose(fout);
     return r;

@@ -98,10 +98,6 @@ struct fcx_ctx {
     uint64_t *blk_off = nullptr;
     uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits
     uint64_t *host_words = nullptr;    // pinned mirror
-    // host path staging
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    uint64_t d_in_cap = 0, d_out_cap = 0;
-    hipStream_t own_stream = nullptr;
     // profiling
     bool profiling = false;
     hipEvent_t ev[kNumStages + 1] = {};
@@ -225,9 +221,6 @@ void fcx_ctx_destroy(fcx_ctx *c) {
     free_scratch(c);
     if (c->dev_words) (void)hipFree(c->dev_words);
     if (c->host_words) (void)hipHostFree(c->host_words);
-    if (c->d_in) (void)hipFree(c->d_in);
-    if (c->d_out) (void)hipFree(c->d_out);
-    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     for (int i = 0; i <= kNumStages; i++)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     delete c;
@@ -336,40 +329,11 @@ int fcx_ctx_stats(fcx_ctx *c, uint64_t *tokens, uint64_t *matches, uint64_t *laz
     return FCX_OK;
 }
 
-int fcx_compress_host(fcx_ctx *c, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len) {
-    if (!c || (!in && n) || !out) return fail(FCX_ERR_ARG, "fcx_compress_host: NULL argument");
-    HIP_TRY(hipSetDevice(c->device));
-    if (!c->own_stream) HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-    const uint64_t shard = c->cap_n ? c->cap_n : c->B;
-    const uint64_t need_in = n < shard ? n : shard;
-    const uint64_t need_out = fcx_shard_bound(need_in, c->B);
-    if (c->d_in_cap < need_in) {
-        if (c->d_in) (void)hipFree(c->d_in);
-        c->d_in = nullptr;
-        int r = dalloc(&c->d_in, need_in, "d_in");
-        if (r) return r;
-        c->d_in_cap = need_in;
-    }
-    if (c->d_out_cap < need_out) {
-        if (c->d_out) (void)hipFree(c->d_out);
-        c->d_out = nullptr;
-        int r = dalloc(&c->d_out, need_out, "d_out");
-        if (r) return r;
-        c->d_out_cap = need_out;
-    }
-    uint64_t o = 0;
-    for (uint64_t off = 0; off < n; off += shard) {
-        const uint64_t len = n - off < shard ? n - off : shard;
-        HIP_TRY(hipMemcpyAsync(c->d_in, in + off, len, hipMemcpyHostToDevice, c->own_stream));
-        uint64_t got = 0;
-        int r = fcx_compress_shard(c, c->d_in, len, c->d_out, c->d_out_cap, &got, c->own_stream);
-        if (r) return r;
-        if (o + got > cap) return fail(FCX_ERR_CAPACITY, "fcx_compress_host: output capacity too small");
-        HIP_TRY(hipMemcpyAsync(out + o, c->d_out, got, hipMemcpyDeviceToHost, c->own_stream));
-        HIP_TRY(hipStreamSynchronize(c->own_stream));
-        o += got;
-    }
-    if (out_len) *out_len = o;
+int fcx_ctx_info(fcx_ctx *c, int *device, uint32_t *block_bytes, uint64_t *shard_bytes) {
+    if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
+    if (device) *device = c->device;
+    if (block_bytes) *block_bytes = c->B;
+    if (shard_bytes) *shard_bytes = c->cap_n ? c->cap_n : c->B;
     return FCX_OK;
 }
 

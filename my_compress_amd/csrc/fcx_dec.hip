@@ -777,6 +777,28 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
         }
         uint32_t mtot;
         uint32_t rank = mc + block_xscan(nm, sh, &mtot);
+        if (mtot == 0) {
+            // literal tokens only (random data): the bytes are the chars, one per token
+            const uint32_t cnt = limit - tc;
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++)
+                if (valid[u]) o[oc + 4 * tid + u] = (uint8_t)c[u];
+            // history = the last 2 KiB of [history | these bytes]
+            uint8_t h[kHist / kDLzThreads];
+#pragma unroll
+            for (uint32_t q = 0; q < kHist / kDLzThreads; q++) {
+                const uint32_t j = cnt + tid + q * kDLzThreads;   // index in [history | bytes]
+                h[q] = j < kHist ? ob[j] : ch[tc + j - kHist];
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t q = 0; q < kHist / kDLzThreads; q++) ob[tid + q * kDLzThreads] = h[q];
+            __syncthreads();
+            oc += cnt;
+            tc += cnt;
+            window = 4 * kDLzThreads;
+            continue;
+        }
         uint32_t lsum = 0;
 #pragma unroll
         for (uint32_t u = 0; u < 4; u++) {
@@ -948,9 +970,6 @@ struct fcx_dctx {
     uint64_t *words = nullptr;        // [0] total out, [1] error bits, [2] symbol bytes, [3] golomb values,
                                       // [4..7] Jacobi rounds / serial fallbacks (symbols, golomb)
     uint64_t *host_words = nullptr;
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    uint64_t d_in_cap = 0, d_out_cap = 0;
-    hipStream_t own = nullptr;
     bool profiling = false, timed = false;
     hipEvent_t ev[kDStages + 1] = {};
 };
@@ -994,11 +1013,10 @@ void fcx_dctx_destroy(fcx_dctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
-    void *ptrs[] = {c->blk, c->ds, c->symb, c->tbl, c->child, c->sym, c->glen, c->words, c->d_in, c->d_out};
+    void *ptrs[] = {c->blk, c->ds, c->symb, c->tbl, c->child, c->sym, c->glen, c->words};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (c->host_words) (void)hipHostFree(c->host_words);
-    if (c->own) (void)hipStreamDestroy(c->own);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     delete c;
@@ -1083,41 +1101,9 @@ int fcx_decompress_shard(fcx_dctx *c, const uint8_t *d_in, uint64_t in_len, uint
     return FCX_OK;
 }
 
-int fcx_decompress_host(fcx_dctx *c, const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t cap,
-                        uint64_t *out_len) {
-    if (!c || !in || (cap && !out)) return dfail(FCX_ERR_ARG, "fcx_decompress_host: NULL argument");
-    if (in_len < FCX_HEADER_BYTES || memcmp(in, "FCX7", 4) != 0) return dfail(FCX_ERR_FORMAT, "not an FCX7 stream");
-    DHIP(hipSetDevice(c->device));
-    if (!c->own) DHIP(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
-    // walk the records on the host (the u16 block count of the header wraps) and
-    // decode groups of up to 1024 blocks (<= 1 GiB of output) per device call
-    const uint8_t *body = in + FCX_HEADER_BYTES;
-    const uint64_t blen = in_len - FCX_HEADER_BYTES;
-    uint64_t pos = 0, o = 0;
-    while (pos < blen) {
-        uint64_t g0 = pos;
-        uint32_t nb = 0;
-        while (pos < blen && nb < 1024) {
-            if (blen - pos < 4) return dfail(FCX_ERR_FORMAT, "truncated block record");
-            uint32_t L;
-            memcpy(&L, body + pos, 4);
-            if (L > blen - pos - 4) return dfail(FCX_ERR_FORMAT, "truncated block record");
-            pos += 4 + (uint64_t)L;
-            nb++;
-        }
-        const uint64_t glen_in = pos - g0, gcap = (uint64_t)nb * FCX_MAX_BLOCK_BYTES;
-        int r;
-        if ((r = dgrow(&c->d_in, c->d_in_cap, glen_in, "d_in"))) return r;
-        if ((r = dgrow(&c->d_out, c->d_out_cap, gcap, "d_out"))) return r;
-        DHIP(hipMemcpyAsync(c->d_in, body + g0, glen_in, hipMemcpyHostToDevice, c->own));
-        uint64_t got = 0;
-        if ((r = fcx_decompress_shard(c, c->d_in, glen_in, nb, c->d_out, gcap, &got, c->own))) return r;
-        if (o + got > cap) return dfail(FCX_ERR_CAPACITY, "fcx_decompress_host: output capacity too small");
-        DHIP(hipMemcpyAsync(out + o, c->d_out, got, hipMemcpyDeviceToHost, c->own));
-        DHIP(hipStreamSynchronize(c->own));
-        o += got;
-    }
-    if (out_len) *out_len = o;
+int fcx_dctx_device(fcx_dctx *c, int *device) {
+    if (!c) return dfail(FCX_ERR_ARG, "NULL ctx");
+    if (device) *device = c->device;
     return FCX_OK;
 }
 
