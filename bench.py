@@ -79,6 +79,9 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages, block=None
     host = make_shard(kind, seed, rank, n)
     gen_s = time.time() - t
     d_in = host.to(dev)
+    host_path = None
+    if world == 1 and args.host_path and kind == args.kind:
+        host_path = host_leg(host, n, block)
     del host
     cap = mc.shard_bound(n, block)
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
@@ -116,6 +119,7 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages, block=None
         "seconds": dt, "ms_per_step": dt / args.steps * 1e3,
         "value": world * n * args.steps / dt / 1e6, "gen_s": gen_s,
         "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
+        "host_path": host_path,
     }
     stats = ctx.stats()
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
@@ -137,6 +141,34 @@ def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages, block=None
     del d_in, d_out
     torch.cuda.empty_cache()
     return res, concat
+
+
+def host_leg(host, n, block, reps=3):
+    """host-to-host rate (PCIe in both directions, pinned buffers, 256 MiB shards
+    through the pipelined fcx_compress_stream path): reported beside `value`, never as it"""
+    import ctypes
+
+    import my_compress_amd as mc
+
+    shard = (256 << 20) // block * block
+    ctx = mc.Context(0, block, shard)
+    cap = mc.shard_bound(n, block)
+    out = ctypes.create_string_buffer(cap)
+    got = ctypes.c_uint64(0)
+    src = ctypes.cast(host.data_ptr(), ctypes.POINTER(ctypes.c_uint8))
+    try:
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            mc._check(mc.lib().fcx_compress_host(ctx._h, src, n, ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)),
+                                                 cap, ctypes.byref(got)), "fcx_compress_host")
+            ts.append(time.perf_counter() - t0)
+    finally:
+        ctx.close()
+    dt = min(ts)
+    return {"value": n / dt / 1e6, "unit": "MB/s", "ms": dt * 1e3, "out_bytes": got.value,
+            "note": "host memory in -> host memory out, 256 MiB shards, H2D/compute/D2H overlapped; "
+                    "the output lands in pageable memory (one extra host copy)"}
 
 
 def decode_leg(d_rec, rec_len, n, block, d_in, args, dev, dist, world):
@@ -302,6 +334,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the GPU decoder timing")
+    ap.add_argument("--no-host-path", dest="host_path", action="store_false",
+                    help="skip the host-to-host (PCIe-inclusive) timing of the main leg")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     args = ap.parse_args()
@@ -371,6 +405,7 @@ def main():
             "lazy_evals": main_res["lazy_evals"],
             "concat": concat,
             "decode": main_res.get("decode"),
+            "host_path": main_res.get("host_path"),
         }
         for name, lr in legs.items():
             line[name] = {k: lr[k] for k in ["value", "ms_per_step", "ratio", "block_bytes", "stages_ms", "lazy_evals"]}
