@@ -14,7 +14,7 @@
 
 namespace fcx {
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                  uint64_t *chain_pfx, uint32_t *tinfo, hipStream_t st);
+                  uint64_t *chain_pfx, uint32_t *tinfo, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx,
                   const uint32_t *tinfo, uint64_t *fp, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -326,6 +326,19 @@ int fcx_ctx_stats(fcx_ctx *c, uint64_t *tokens, uint64_t *matches, uint64_t *laz
         for (auto &x : bi) tl += (x.len + kTile - 1) / kTile;
         *tiles = tl;
     }
+    return FCX_OK;
+}
+
+// development only (not in fcx.h): the match kernel alone with experiment bits, for
+// per-phase timing (tools/matchphase.py); the context's scratch is left invalid
+int fcx_debug_match(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint32_t dbg, void *stream) {
+    if (!c || !d_in || n == 0) return fail(FCX_ERR_ARG, "fcx_debug_match: bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    int r = ensure_scratch(c, n);
+    if (r) return r;
+    const Layout L = make_layout(n, c->B);
+    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, (hipStream_t)stream, dbg);
+    HIP_TRY(hipGetLastError());
     return FCX_OK;
 }
 

@@ -46,10 +46,24 @@ __device__ inline void chunk_of(const Layout &L, uint32_t r, uint32_t &s, uint32
 
 // ---------------------------------------------------------------------------
 __device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32_t i1, uint32_t *out32 /*8 words*/) {
-    // loads the (up to) 32 symbols [i0, i1) as 8 words, masked past i1
+    // loads the (up to) 32 symbols [i0, i1) as two 16-B loads (i0 is a multiple of 32
+    // and stream strides are multiples of 16; the buffers carry slack past the end),
+    // bytes past i1 zeroed
     const uint32_t n = i1 > i0 ? i1 - i0 : 0;
+    if (n == 0) {
 #pragma unroll
-    for (uint32_t q = 0; q < 8; q++) out32[q] = (4 * q < n) ? w4[(i0 >> 2) + q] : 0u;
+        for (uint32_t q = 0; q < 8; q++) out32[q] = 0;
+        return 0;
+    }
+    const uint4 a = ((const uint4 *)(w4 + (i0 >> 2)))[0], b = ((const uint4 *)(w4 + (i0 >> 2)))[1];
+    out32[0] = a.x; out32[1] = a.y; out32[2] = a.z; out32[3] = a.w;
+    out32[4] = b.x; out32[5] = b.y; out32[6] = b.z; out32[7] = b.w;
+    if (n < 32)
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t lo = 4 * q;
+            out32[q] = lo >= n ? 0u : (n - lo >= 4 ? out32[q] : out32[q] & ((1u << (8 * (n - lo))) - 1u));
+        }
     return n;
 }
 
@@ -320,11 +334,50 @@ __global__ __launch_bounds__(256) void k_encode(Layout L, const BlockInfo *__res
     const uint32_t hb = (b * kStreams + s) * 256;
     ct[tid] = ctab[hb + tid];
     lt[tid] = ltab[hb + tid];
-    __syncthreads();
+    // all 256 symbols with 8-bit codes (the chars of random data): the code stream is a
+    // byte substitution at a byte-aligned offset
+    const bool byte8 = __syncthreads_and(lt[tid] == 8) != 0;
     const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
     const uint32_t i0 = c0 + 32 * tid, i1 = min(c1, i0 + 32);
     uint32_t sym[8];
     const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
+    if (byte8) {
+        const uint64_t g0 = 8 * (blk_off[b] + bi.words_rel[s]) + chunk_off[(uint64_t)b * L.cpb_total + r];
+        const uint32_t sh0 = (uint32_t)(g0 & 31), nw = (sh0 + 8 * (c1 - c0) + 31) >> 5;
+        for (uint32_t x = tid; x < nw; x += 256) ws[x] = 0;
+        uint32_t v[9];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t w = sym[q];
+            v[q] = ct[w & 0xFF] | (ct[(w >> 8) & 0xFF] << 8) | (ct[(w >> 16) & 0xFF] << 16) | (ct[w >> 24] << 24);
+            if (4 * q >= n) v[q] = 0;
+            else if (n - 4 * q < 4) v[q] &= (1u << (8 * (n - 4 * q))) - 1u;
+        }
+        // this lane's bytes start at staging byte sh0/8 + 32 tid: shift into 9 words,
+        // the first and last shared with the neighbouring lanes
+        const uint32_t bo = (sh0 >> 3) + 32 * tid, sb = 8 * (bo & 3), w0 = bo >> 2;
+        v[8] = 0;
+        __syncthreads();
+        if (n) {
+            uint32_t prev = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 9; q++) {
+                const uint32_t cur = v[q];
+                const uint32_t o = sb ? (cur << sb) | (prev >> (32 - sb)) : cur;
+                prev = cur;
+                if (q == 0 || q >= 7) { if (o) atomicOr(&ws[w0 + q], o); }
+                else ws[w0 + q] = o;
+            }
+        }
+        __syncthreads();
+        uint32_t *o32 = (uint32_t *)out + (g0 >> 5);
+        for (uint32_t x = tid; x < nw; x += 256) {
+            const uint32_t val = ws[x];
+            if (x == 0 || x == nw - 1) { if (val) atomicOr(&o32[x], val); }
+            else o32[x] = val;
+        }
+        return;
+    }
     uint32_t nb = 0;
     for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
     // block exclusive scan of nb

@@ -265,6 +265,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     __syncthreads();
     const bool rmode = (s_nruns <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
+    if (dbg & 16u) return;   // timing: staging + run count only
 
     if (rmode) {
         for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
@@ -321,6 +322,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         }
     __syncthreads();
 
+    if (dbg & 32u) return;   // timing: + counting sort
     // ---- 3. queries: position i = w0 + q0 + tid + kMT*r, kIlp at a time ----
     // per walk: range (start | len << 16), packed best = L << 13 | (8191 - position),
     // query bytes 0..11, x | cap << 13 | tag3 << 22
@@ -411,6 +413,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         dense_phase(sdw, region, step, s_red, &s_unknown, m + bstart + w0,
                     rmode ? mbits + (uint64_t)b * L.wpb + (w0 >> 6) : nullptr, q0, npos, nload, blen - w0, w0);
 
+    if (dbg & 64u) return;   // timing: + queries (no parse)
     uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
     uint32_t *ti = tinfo + 8ull * blockIdx.x;
     const uint32_t nwords = (t1 - t0 + 63) / 64;
@@ -520,10 +523,12 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 }
 
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
-                  uint32_t *tinfo, hipStream_t st) {
+                  uint32_t *tinfo, hipStream_t st, uint32_t dbg_override) {
     // FCX_MATCH_DBG (experiments only): bit0 skip searches, bit1 skip long extension (both: output invalid),
-    // bit2 never / bit3 always take the whole-tile run mode (output stays exact)
-    static const uint32_t dbg = getenv("FCX_MATCH_DBG") ? (uint32_t)atoi(getenv("FCX_MATCH_DBG")) : 0u;
+    // bit2 never / bit3 always take the whole-tile run mode (output stays exact); bits 4-6 (phase exits)
+    // only through fcx_debug_match, which launches this kernel alone
+    static const uint32_t env = getenv("FCX_MATCH_DBG") ? (uint32_t)atoi(getenv("FCX_MATCH_DBG")) & 15u : 0u;
+    const uint32_t dbg = dbg_override != ~0u ? dbg_override : env;
     const uint32_t grid = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, dbg);
 }
