@@ -505,18 +505,49 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     for (uint32_t w = tid; w < kFlagW; w += 256) lf[w] = 0;
     for (uint32_t w = tid; w < kPW; w += 256) lp[w] = 0;
     for (uint32_t w = tid; w < kGW; w += 256) lg[w] = 0;
-    __syncthreads();
+    for (uint32_t w = tid; w < kCharW; w += 256) lc[w] = 0;
 
     const uint8_t *d = in + bstart;
     uint8_t *lcb = (uint8_t *)lc;
+    // the lane's 16 input bytes in one 16-B load: every literal char comes from here
+    uint32_t in4[4];
+    if (s + 16 <= blen && (((uintptr_t)(d + s)) & 15) == 0) {
+        const uint4 v4 = *(const uint4 *)(d + s);
+        in4[0] = v4.x; in4[1] = v4.y; in4[2] = v4.z; in4[3] = v4.w;
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            uint32_t w = 0;
+            for (uint32_t j = 0; j < 4; j++)
+                if (s + 4 * q + j < t1) w |= (uint32_t)d[s + 4 * q + j] << (8 * j);
+            in4[q] = w;
+        }
+    }
+    __syncthreads();
     uint32_t fl = 0, nt_lane = 0;
     uint64_t pacc = 0;
     uint32_t np_lane = 0;
+    if (bits == 0xFFFFu && nm_lane == 0) {
+        // 16 literal tokens: the chars are the input bytes; shifted dword stores into the
+        // staging, the two words shared with the neighbouring lanes by atomicOr
+        const uint32_t bo = tokA - 4 * cw0, sb = 8 * (bo & 3), w0 = bo >> 2;
+        uint32_t prev = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 5; q++) {
+            const uint32_t cur = q < 4 ? in4[q] : 0u;
+            const uint32_t o = sb ? (cur << sb) | (prev >> (32 - sb)) : cur;
+            prev = cur;
+            if (q == 0 || q >= 3) { if (o) atomicOr(&lc[w0 + q], o); }
+            else lc[w0 + q] = o;
+        }
+        fl = 0xFFFFu;
+        nt_lane = 16;
+    } else
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
         if ((bits >> q) & 1u) {
             const uint32_t Lm = m_len(mm[q]);
-            lcb[tokA + nt_lane - 4 * cw0] = d[s + q + Lm];
+            lcb[tokA + nt_lane - 4 * cw0] = Lm ? d[s + q + Lm] : (uint8_t)(in4[q >> 2] >> (8 * (q & 3)));
             if (Lm == 0) {
                 fl |= 1u << nt_lane;
             } else {
