@@ -204,6 +204,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     uint16_t *h16 = (uint16_t *)region;
     uint16_t *ent = (uint16_t *)(region + kHeadWords);     // window entries, bucket-sorted
     __shared__ uint32_t s_unknown;
+    __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
     __shared__ uint32_t s_nruns;
     __shared__ uint32_t s_chg[2];
     __shared__ uint32_t s_red[3 * kWaves];   // cross-wave scan partials
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             sdw[x] = v;
         }
     }
-    if (tid == 0) { s_unknown = 0; s_nruns = 0; s_chg[0] = 0; s_chg[1] = 0; }
+    if (tid == 0) { s_unknown = 0; s_match = 0; s_nruns = 0; s_chg[0] = 0; s_chg[1] = 0; }
     __syncthreads();
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
@@ -249,19 +250,29 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // ---- 1b. run count of the image: a tile of long runs (zeros, runs) skips the
     // bucket search and takes every match from the run table (dense_phase) ----
     {
-        // per dword: bytes differing from their predecessor (byte 0 of the image counts once)
-        uint32_t cnt = tid == 0 && nload > 0 ? 1u : 0u;
-        for (uint32_t w = tid; 4 * w < nload; w += kMT) {
+        // per dword: bytes differing from their predecessor (byte 0 of the image counts
+        // once).  The first 2 KiB decide most tiles: more than kRunTile runs there
+        // already rules the run mode out (random data, text), so the rest is skipped.
+        auto runs_in = [&](uint32_t w) -> uint32_t {
+            if (4 * w >= nload) return 0u;
             const uint32_t v = sdw[w], pv = w ? sdw[w - 1] : v << 24;
             uint32_t x = v ^ ((v << 8) | (pv >> 24));
             x |= x >> 4; x |= x >> 2; x |= x >> 1;
             uint32_t msk = x & 0x01010101u;
             const uint32_t nb = nload - 4 * w;
             if (nb < 4) msk &= (1u << (8 * nb)) - 1u;
-            cnt += (uint32_t)__builtin_popcount(msk);
-        }
+            return (uint32_t)__builtin_popcount(msk);
+        };
+        uint32_t cnt = (tid == 0 && nload > 0 ? 1u : 0u) + runs_in(tid);
         cnt = wave_sum_u32(cnt);
         if ((tid & 63) == 0) atomicAdd(&s_nruns, cnt);
+        __syncthreads();
+        if (s_nruns <= kRunTile) {
+            cnt = 0;
+            for (uint32_t w = tid + kMT; 4 * w < nload; w += kMT) cnt += runs_in(w);
+            cnt = wave_sum_u32(cnt);
+            if ((tid & 63) == 0 && cnt) atomicAdd(&s_nruns, cnt);
+        }
     }
     __syncthreads();
     const bool rmode = (s_nruns <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
@@ -279,7 +290,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // 16-bit counters, two per dword (a bucket never exceeds 6144 entries)
     const uint32_t ins_end = min(npos, blen >= 3 ? blen - 2 - w0 : 0);  // j + 3 <= blen
     constexpr uint32_t kIns = (kWinPos + kMT - 1) / kMT;               // 12 per lane
-    uint32_t ins_hr[kIns];                                             // bucket << 16 | rank
+    uint32_t ins_hr[kIns];                                             // bucket << 16 | tag << 13 | rank
 #pragma unroll
     for (uint32_t r = 0; r < kIns; r++) {
         const uint32_t x = tid + kMT * r;
@@ -288,7 +299,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             const uint32_t h = key_mix(lds_key3(sdw, x));
             const uint32_t bk = h >> 12, sh = 16 * (bk & 1);
             const uint32_t old = atomicAdd(&hw[bk >> 1], 1u << sh);
-            ins_hr[r] = (bk << 16) | ((old >> sh) & 0xFFFFu);
+            ins_hr[r] = (bk << 16) | ((h & 7u) << 13) | ((old >> sh) & 0x1FFFu);   // rank < 6144
         }
     }
     __syncthreads();
@@ -317,8 +328,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if (ins_hr[r] != 0xFFFFFFFFu) {
             const uint32_t x = tid + kMT * r;
             const uint32_t bk = ins_hr[r] >> 16;
-            const uint32_t h = key_mix(lds_key3(sdw, x));
-            ent[h16[bk] + (ins_hr[r] & 0xFFFFu)] = (uint16_t)(((h & 7u) << 13) | x);
+            ent[h16[bk] + (ins_hr[r] & 0x1FFFu)] = (uint16_t)((ins_hr[r] & 0xE000u) | x);
         }
     __syncthreads();
 
@@ -396,6 +406,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             // stored (whole 256-B rows, zeros included) only by waves that found a match
             const uint64_t mb = __ballot(res != 0);
             if (mb && x < npos) m[bstart + w0 + x] = res;
+            if (mb && (tid & 63) == 0) s_match = 1;
             const uint32_t xw = q0 + (tid & ~63u) + kMT * (g + u);
             if ((tid & 63) == 0 && xw < npos) mbits[(uint64_t)b * L.wpb + ((w0 + xw) >> 6)] = mb;
             const uint32_t q = g + u;
@@ -409,7 +420,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }   // bucket search
 
     // ---- 3b. dense windows: exact matches of the unknown positions over the run table ----
-    if (s_unknown != 0)
+    const bool dense = s_unknown != 0;   // matches may come from the run table: no fast path below
+    if (dense)
         dense_phase(sdw, region, step, s_red, &s_unknown, m + bstart + w0,
                     rmode ? mbits + (uint64_t)b * L.wpb + (w0 >> 6) : nullptr, q0, npos, nload, blen - w0, w0);
 
@@ -430,6 +442,13 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     const uint32_t s = t0 + tid * kSeg;
     const uint32_t se = min(s + kSeg, t1);
     uint32_t V = 0, X = s;
+    uint32_t T = 0;
+    uint32_t *Ys = Vs;   // exits of a Jacobi round (Vs is free until the counts below)
+    if (s_match == 0 && !dense) {
+        // no match anywhere (most tiles of random data): every position is a literal token
+        if (s < t1) T = se - s == 32 ? ~0u : ((1u << (se - s)) - 1u);
+        if (tid == 0) Gs[(t1 - t0 + kSeg - 1) / kSeg] = t1;
+    } else {
     if (s < t1) {
         uint32_t t = s;
         while (t < se) { V |= 1u << (t - s); t += step[t - t0]; }
@@ -443,8 +462,6 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // entry of segment k + 1 is the exit of the nearest active segment <= k (a
     // block-wide running max of active indices), so a long token passes over any
     // number of segments in one round.
-    uint32_t T = 0;
-    uint32_t *Ys = Vs;   // exits of this round (Vs is free until the counts below)
     for (uint32_t r = 0;; r++) {
         const uint32_t e = Gs[tid];
         uint32_t ex;
@@ -476,6 +493,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         __syncthreads();
         if (!s_chg[r & 1]) break;
     }
+    }   // Jacobi
     // counts of this lane's chain positions, prefix over lanes
     uint32_t cnt[3] = {(uint32_t)__builtin_popcount(T), 0, 0};
     for (uint32_t bits = T; bits; bits &= bits - 1) {
