@@ -20,7 +20,8 @@
 //                  (chunk histogram . code lengths) - no second pass over the data
 //   k_block_layout record layout and size per block
 //   k_scan_blocks  record offsets across the shard (+ capacity check)
-//   k_zero         zero the output bytes the encoder ORs into
+//   k_zero_edges   zero the words the encoder ORs into (the two edge words of every
+//                  chunk; every other output byte is stored whole by k_encode or k_headers)
 //   k_encode       each lane packs its 32 codes into whole words (LDS atomics only
 //                  for the two words it shares with neighbours); the chunk's words
 //                  are stored at the record's (unaligned) byte offset: interior
@@ -299,15 +300,30 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t nblocks, const Bl
     }
 }
 
-__global__ __launch_bounds__(256) void k_zero(uint8_t *__restrict__ out, const uint64_t *__restrict__ total,
-                                              const uint32_t *__restrict__ err) {
+__global__ __launch_bounds__(256) void k_zero_edges(Layout L, const BlockInfo *__restrict__ binfo,
+                                                    const uint32_t *__restrict__ chunk_off,
+                                                    const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
+                                                    const uint32_t *__restrict__ err) {
     if (*err & kErrCapacity) return;
-    const uint64_t n = *total;
-    const uint64_t n16 = n >> 4;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint4 *o16 = (uint4 *)out;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) o16[i] = make_uint4(0, 0, 0, 0);
-    if (blockIdx.x == 0 && threadIdx.x < (n & 15)) out[(n16 << 4) + threadIdx.x] = 0;
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (uint64_t)L.nblocks * L.cpb_total) return;
+    const uint32_t b = (uint32_t)(q / L.cpb_total), r = (uint32_t)(q % L.cpb_total);
+    uint32_t s, c;
+    chunk_of(L, r, s, c);
+    const BlockInfo &bi = binfo[b];
+    const uint32_t len = bi.slen[s], c0 = c * kChunk;
+    if (!stream_active(bi, s) || c0 >= len) return;
+    const uint64_t base = 8 * (blk_off[b] + bi.words_rel[s]);
+    const uint64_t g0 = base + chunk_off[q];
+    uint32_t *o32 = (uint32_t *)out;
+    if (c0 + kChunk < len) {   // the chunk ends where the next one starts
+        const uint64_t g1 = base + chunk_off[q + 1];
+        o32[g0 >> 5] = 0;
+        if (g1 > g0) o32[(g1 - 1) >> 5] = 0;
+    } else {                   // last chunk: every word through the end of the stream's words
+        const uint64_t g1 = base + 32ull * bi.nwords[s];
+        for (uint64_t w = g0 >> 5; w <= (g1 > g0 ? (g1 - 1) >> 5 : g0 >> 5); w++) o32[w] = 0;
+    }
 }
 
 constexpr uint32_t kEncWords = kChunk + 2;  // codes <= 32 bits
@@ -471,7 +487,8 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
     if (ev) (void)hipEventRecord(ev[2], st);
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, L.nblocks, binfo, blk_off, total, cap, err);
     if (ev) (void)hipEventRecord(ev[3], st);
-    hipLaunchKernelGGL(k_zero, dim3(2048), dim3(256), 0, st, out, total, err);
+    hipLaunchKernelGGL(k_zero_edges, dim3((nchunks + 255) / 256), dim3(256), 0, st, L, binfo, chunk_off, blk_off, out,
+                       err);
     if (ev) (void)hipEventRecord(ev[4], st);
     hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, chunk_off,
                        blk_off, out, err);
