@@ -128,6 +128,7 @@ __global__ __launch_bounds__(64) void k_tree(Layout L, const uint32_t *__restric
     const uint32_t nch = (bi.slen[s] + kChunk - 1) / kChunk;
     const uint32_t *hc = hist + ((uint64_t)b * L.cpb_total + r0) * 256;   // this stream's chunk histograms
     uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll 8
     for (uint32_t c = 0; c < nch; c++)
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) acc[q] += hc[c * 256 + lane + 64 * q];
