@@ -16,7 +16,7 @@ constexpr uint32_t kPBits = 11;     // P_BITS
 constexpr uint32_t kTile = 4096;            // positions per match-kernel workgroup
 constexpr uint32_t kMatchThreads = 512;
 constexpr uint32_t kSubSeg = kTile / kMatchThreads;  // 8 positions per lane in the tile parse
-constexpr uint32_t kHashBits = 12;
+constexpr uint32_t kHashBits = 13;
 constexpr uint32_t kHalo = kWin;                     // left halo of a tile
 constexpr uint32_t kLookAhead = 260;                 // right look-ahead bytes (>= 257)
 constexpr uint32_t kTileBytes = 6464;                // >= kHalo + kTile + kLookAhead, x64
@@ -135,7 +135,6 @@ __device__ inline uint32_t lds_match_len(const uint32_t *w, uint32_t a, uint32_t
     return L;
 }
 
-__device__ inline uint32_t hash3(uint32_t key) { return (key * 2654435761u) >> (32 - kHashBits); }
 
 // ---- exact match over the run decomposition (dense windows: zeros, runs) ----
 // Runs of equal bytes in an LDS byte image are described by a boundary bitmap

@@ -9,7 +9,7 @@
 //
 //   1. stage [t0-2048, t1+260) of the block in LDS (dword loads);
 //   2. counting-sort every window position by the bucket of its 3-byte key (a
-//      bijection of Z/2^24 gives a 12-bit bucket; 16-bit entries keep the position
+//      bijection of Z/2^24 gives a 13-bit bucket; 16-bit entries keep the position
 //      and 3 more hash bits, the rare collisions are rejected by comparing key
 //      bytes); a bucket is one contiguous LDS range (16-bit counters by LDS
 //      atomics, block scan, scatter);
@@ -297,16 +297,17 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         ins_hr[r] = 0xFFFFFFFFu;
         if (x < ins_end) {
             const uint32_t h = key_mix(lds_key3(sdw, x));
-            const uint32_t bk = h >> 12, sh = 16 * (bk & 1);
+            const uint32_t bk = h >> (24 - kHashBits), sh = 16 * (bk & 1);
             const uint32_t old = atomicAdd(&hw[bk >> 1], 1u << sh);
             ins_hr[r] = (bk << 16) | ((h & 7u) << 13) | ((old >> sh) & 0x1FFFu);   // rank < 6144
         }
     }
     __syncthreads();
-    {   // exclusive scan of the 4096 bucket counts: 8 consecutive buckets (4 dwords) per lane
-        uint32_t cw4[4], sum = 0;
+    {   // exclusive scan of the bucket counts: kBkDw consecutive counter dwords per lane
+        constexpr uint32_t kBkDw = (1u << kHashBits) / 2 / kMT;
+        uint32_t cw4[kBkDw], sum = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) { cw4[q] = hw[tid * 4 + q]; sum += (cw4[q] & 0xFFFFu) + (cw4[q] >> 16); }
+        for (uint32_t q = 0; q < kBkDw; q++) { cw4[q] = hw[tid * kBkDw + q]; sum += (cw4[q] & 0xFFFFu) + (cw4[q] >> 16); }
         const uint32_t inc = wave_incl_scan(sum);
         const uint32_t lane = tid & 63, wv = tid >> 6;
         if (lane == 63) s_red[wv] = inc;
@@ -314,12 +315,12 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         uint32_t run = inc - sum;
         for (uint32_t w = 0; w < wv; w++) run += s_red[w];
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
+        for (uint32_t q = 0; q < kBkDw; q++) {
             const uint32_t lo = run, hi = run + (cw4[q] & 0xFFFFu);
             run = hi + (cw4[q] >> 16);
-            hw[tid * 4 + q] = lo | (hi << 16);
+            hw[tid * kBkDw + q] = lo | (hi << 16);
         }
-        if (tid == kMT - 1) hw[(1u << kHashBits) / 2] = run;   // start[4096] = total
+        if (tid == kMT - 1) hw[(1u << kHashBits) / 2] = run;   // start[nbuckets] = total
     }
     __syncthreads();
     // scatter into bucket order: entry = position | 3 more hash bits << 13
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     qb[u] = lds_ld4(sdw, x + 4);
                     qc[u] = lds_ld4(sdw, x + 8);
                     const uint32_t h = key_mix(qa[u] & 0xFFFFFFu);
-                    const uint32_t bk = h >> 12;
+                    const uint32_t bk = h >> (24 - kHashBits);
                     const uint32_t lo = h16[bk], n = h16[bk + 1] - lo;
                     xpk[u] = x | (cap << 13) | ((h & 7u) << 22);
                     if (n > kMaxChainSteps) rng[u] = 0xFFFFFFFFu;
