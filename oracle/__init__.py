@@ -113,3 +113,120 @@ def ref_compress_file(data: bytes, block: int) -> bytes:
         n = R.ref_compress_block(blk, len(blk), ob)
         out += struct.pack("<I", n) + ob.raw[:n]
     return bytes(out)
+
+
+# ---- -c lz78 (lz78_oracle.c; reference my_compress.cpp:1832-1934, 3127-3710) ----
+def _lz78_bind(L):
+    if getattr(L, "_lz78", False):
+        return L
+    L.orc_lz78_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    L.orc_lz78_parse.restype = ctypes.c_uint32
+    L.orc_lz78_compress_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p]
+    L.orc_lz78_compress_block.restype = ctypes.c_uint32
+    L.orc_lz78_decompress_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+    L.orc_lz78_decompress_block.restype = ctypes.c_int64
+    L.orc_lz78_compress_file.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.c_uint64]
+    L.orc_lz78_compress_file.restype = ctypes.c_uint64
+    L.orc_lz78_decompress_file.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+    L.orc_lz78_decompress_file.restype = ctypes.c_int64
+    L._lz78 = True
+    return L
+
+
+def lz78_bound(n: int, block: int) -> int:
+    """output capacity for an FCX8 file: ≤ 4 B per input byte + 64 KiB per block"""
+    nb = max(1, (n + block - 1) // block)
+    return 10 + 4 * n + (65536 + 4) * nb
+
+
+def lz78_parse(data: bytes):
+    n = len(data)
+    idx = (ctypes.c_uint32 * (n + 1))()
+    c = (ctypes.c_uint8 * (n + 1))()
+    N = _lz78_bind(orc()).orc_lz78_parse(data, n, idx, c)
+    return [(idx[i], c[i]) for i in range(N)]
+
+
+def lz78_compress_block(block: bytes) -> bytes:
+    out = ctypes.create_string_buffer(4 * len(block) + 65536)
+    n = _lz78_bind(orc()).orc_lz78_compress_block(block, len(block), out)
+    return out.raw[:n]
+
+
+def lz78_decompress_block(payload: bytes, cap: int) -> bytes:
+    out = ctypes.create_string_buffer(max(cap, 1))
+    n = _lz78_bind(orc()).orc_lz78_decompress_block(payload, len(payload), out, cap)
+    if n < 0:
+        raise RuntimeError("oracle lz78 decompress failed")
+    return out.raw[:n]
+
+
+def lz78_compress_file(data: bytes, block: int) -> bytes:
+    cap = lz78_bound(len(data), block)
+    out = ctypes.create_string_buffer(cap)
+    n = _lz78_bind(orc()).orc_lz78_compress_file(data, len(data), block, out, cap)
+    if n == 0:
+        raise RuntimeError("oracle lz78 compress failed")
+    return out.raw[:n]
+
+
+def lz78_decompress_file(blob: bytes, cap: int) -> bytes:
+    out = ctypes.create_string_buffer(max(cap, 1))
+    n = _lz78_bind(orc()).orc_lz78_decompress_file(blob, len(blob), out, cap)
+    if n < 0:
+        raise RuntimeError("oracle lz78 decompress failed")
+    return out.raw[:n]
+
+
+def _ref_lz78_bind(R):
+    if getattr(R, "_lz78", False):
+        return R
+    R.ref_lz78_compress_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p]
+    R.ref_lz78_compress_block.restype = ctypes.c_uint32
+    R.ref_lz78_tokens.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    R.ref_lz78_tokens.restype = ctypes.c_uint32
+    R.ref_lz78_decompress_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+    R.ref_lz78_decompress_block.restype = ctypes.c_int64
+    R._lz78 = True
+    return R
+
+
+def ref_lz78_tokens(data: bytes):
+    R = ref()
+    if R is None:
+        raise RuntimeError("oracle/_ref/libref.so not built")
+    n = len(data)
+    idx = (ctypes.c_uint32 * (n + 1))()
+    c = (ctypes.c_uint8 * (n + 1))()
+    N = _ref_lz78_bind(R).ref_lz78_tokens(data, n, idx, c)
+    return [(idx[i], c[i]) for i in range(N)]
+
+
+def ref_lz78_compress_block(block: bytes) -> bytes:
+    R = ref()
+    if R is None:
+        raise RuntimeError("oracle/_ref/libref.so not built")
+    out = ctypes.create_string_buffer(4 * len(block) + 65536)
+    n = _ref_lz78_bind(R).ref_lz78_compress_block(block, len(block), out)
+    return out.raw[:n]
+
+
+def ref_lz78_decompress_block(payload: bytes, cap: int) -> bytes:
+    R = ref()
+    if R is None:
+        raise RuntimeError("oracle/_ref/libref.so not built")
+    out = ctypes.create_string_buffer(max(cap, 1))
+    n = _ref_lz78_bind(R).ref_lz78_decompress_block(payload, len(payload), out, cap)
+    return out.raw[:min(n, cap)]
+
+
+def ref_lz78_compress_file(data: bytes, block: int) -> bytes:
+    """the reference lz78 block encoder framed like main() with -c lz78 ("FCX8")"""
+    import struct
+    nb = (len(data) + block - 1) // block
+    out = bytearray(b"FCX8" + struct.pack("<IH", len(data) & 0xFFFFFFFF, nb & 0xFFFF))
+    for off in range(0, len(data), block):
+        p = ref_lz78_compress_block(data[off:off + block])
+        out += struct.pack("<I", len(p)) + p
+    return bytes(out)

@@ -342,6 +342,10 @@ static uint32_t huffman_stream_decode(const uint8_t *in, uint32_t avail, uint8_t
     return hdr + 4 + 4 * nw;
 }
 
+uint32_t orc_huffman_stream_decode(const uint8_t *in, uint32_t avail, uint8_t *dst, uint32_t count) {
+    return huffman_stream_decode(in, avail, dst, count);
+}
+
 /* ------------------------------------------------------------------------- */
 /* Block codec, my_compress_file_lz77 2115-2253 + make_bitMap_table 2073-2113 */
 uint32_t orc_compress_block(const uint8_t *in, uint32_t len, uint8_t *out, int finder) {

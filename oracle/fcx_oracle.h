@@ -52,6 +52,21 @@ uint64_t orc_compress_file(const uint8_t *in, uint64_t n, uint32_t block_bytes, 
 /* main() decompress loop (my_compress.cpp:4137-4204); returns decoded bytes or -1 */
 int64_t orc_decompress_file(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap);
 
+/* one Huffman sub-stream decoder (huffman_decode_char 930-984 / my_huffman_decode_char
+ * 1107-1187); returns bytes consumed, 0 on malformed input */
+uint32_t orc_huffman_stream_decode(const uint8_t *in, uint32_t avail, uint8_t *dst, uint32_t count);
+
+/* ---- -c lz78 (lz78_oracle.c) ---------------------------------------------- */
+/* my_LZ78_compress (my_compress.cpp:1832-1899): tokens (idx, c); returns N */
+uint32_t orc_lz78_parse(const uint8_t *in, uint32_t len, uint32_t *idx, uint8_t *c);
+/* my_compress_file_lz78 (my_compress.cpp:3127-3476); returns payload bytes */
+uint32_t orc_lz78_compress_block(const uint8_t *in, uint32_t len, uint8_t *out);
+/* my_decompress_file_lz78 (my_compress.cpp:3478-3710); decoded bytes or -1 */
+int64_t orc_lz78_decompress_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap);
+/* main() with -c lz78: "FCX8" file; total bytes or 0 */
+uint64_t orc_lz78_compress_file(const uint8_t *in, uint64_t n, uint32_t block_bytes, uint8_t *out, uint64_t cap);
+int64_t orc_lz78_decompress_file(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

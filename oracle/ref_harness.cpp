@@ -13,6 +13,7 @@
  *   ref_combine_bits    -> combine_bits            (my_compress.cpp:1292)
  *   ref_huffman_tree    -> create_huffman_tree     (my_compress.cpp:535)
  *   ref_huffman_encode_char -> my_huffman_encode_char (my_compress.cpp:987)
+ *   ref_lz78_* (below)      -> the -c lz78 block codec
  */
 #define main ref_main
 #include "my_compress.cpp"
@@ -112,4 +113,48 @@ extern "C" uint32_t ref_huffman_tree(const uint32_t *weights, uint32_t n, uint32
 
 extern "C" uint32_t ref_huffman_encode_char(const uint8_t *src, uint32_t n, uint8_t *out) {
     return my_huffman_encode_char((uInt8 *)src, n, out);
+}
+
+/* ---- -c lz78 ----------------------------------------------------------------
+ *   ref_lz78_compress_block   -> my_compress_file_lz78   (my_compress.cpp:3127)
+ *   ref_lz78_tokens           -> my_LZ78_compress        (my_compress.cpp:1832)
+ *   ref_lz78_decompress_block -> my_decompress_file_lz78 (my_compress.cpp:3478)
+ */
+extern "C" uint32_t ref_lz78_compress_block(const uint8_t *in, uint32_t len, uint8_t *out) {
+    uInt8 *buf = new uInt8[(size_t)len + 4096]();
+    memcpy(buf, in, len);
+    uInt8 *obuf = new uInt8[4 * (size_t)len + 65536]();
+    uInt32 n = my_compress_file_lz78(buf, len, obuf);
+    fflush(stdout);
+    cout.flush();
+    memcpy(out, obuf, n);
+    delete[] buf;
+    delete[] obuf;
+    return n;
+}
+
+extern "C" uint32_t ref_lz78_tokens(const uint8_t *in, uint32_t len, uint32_t *idx, uint8_t *c) {
+    uInt8 *buf = new uInt8[(size_t)len + 4096]();
+    memcpy(buf, in, len);
+    vector<stLZ78CmpCp> toks;
+    my_LZ78_compress(buf, len, &toks);
+    for (size_t i = 0; i < toks.size(); i++) { idx[i] = toks[i].idx; c[i] = toks[i].c; }
+    delete[] buf;
+    return (uint32_t)toks.size();
+}
+
+extern "C" int64_t ref_lz78_decompress_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap) {
+    char *mem = NULL; size_t memlen = 0;
+    FILE *f = open_memstream(&mem, &memlen);
+    uInt8 *buf = new uInt8[(size_t)len + 4096]();
+    memcpy(buf, in, len);
+    uInt32 n = my_decompress_file_lz78(buf, len, f);
+    fflush(stdout);
+    cout.flush();
+    fclose(f);
+    if (memlen < cap) cap = memlen;
+    memcpy(out, mem, cap);
+    free(mem);
+    delete[] buf;
+    return (int64_t)n;
 }
