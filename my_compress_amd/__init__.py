@@ -89,6 +89,12 @@ def lib():
     L.fcx_dctx_stage_count.argtypes = [ctypes.c_void_p]
     L.fcx_dctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                  ctypes.POINTER(ctypes.c_float)]
+    L.fcx_lz78_compress_shard.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+    L.fcx_lz78_compress_host.argtypes = [c_u8p, ctypes.c_uint64, ctypes.c_uint32, c_u8p, ctypes.c_uint64,
+                                         ctypes.POINTER(ctypes.c_uint64)]
+    L.fcx_lz78_compress_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, c_u8p]
+    L.fcx_lz78_compress_block.restype = ctypes.c_uint32
     L.fcx_last_error.restype = ctypes.c_char_p
     L.fcx_version.restype = ctypes.c_char_p
     _lib = L
@@ -318,3 +324,32 @@ def decompress(blob: bytes) -> bytes:
         out.append(my_decompress_file_lz77(blob[off:off + sz]))
         off += sz
     return b"".join(out)
+
+
+# ---- -c lz78 (FCX8): my_compress_file_lz78 (my_compress.cpp:3127-3476) on the GPU ----
+def lz78_bound(n: int, block_bytes: int = BLOCK_BYTES) -> int:
+    """output capacity for compress_lz78: records are <= ~9.1 B per input byte + ~600 B"""
+    nb = (n + block_bytes - 1) // block_bytes
+    return HEADER_BYTES + 10 * n + 4096 * max(nb, 1)
+
+
+def my_compress_file_lz78(block: bytes) -> bytes:
+    """one block (<= 1 MiB) -> payload, same bytes as my_compress_file_lz78 (:3127)"""
+    n = len(block)
+    if n == 0:
+        return b""
+    out = ctypes.create_string_buffer(10 * n + 4096)
+    got = lib().fcx_lz78_compress_block(block, n, out)
+    if got == 0:
+        raise FcxError(f"fcx_lz78_compress_block failed: {lib().fcx_last_error().decode(errors='replace')}")
+    return out.raw[:got]
+
+
+def compress_lz78(data: bytes, block_bytes: int = BLOCK_BYTES) -> bytes:
+    """whole FCX8 file for `data` (main() with -c lz78, :4073-4136)"""
+    cap = lz78_bound(len(data), block_bytes)
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_uint64()
+    _check(lib().fcx_lz78_compress_host(data, len(data), block_bytes, out, cap, ctypes.byref(n)),
+           "fcx_lz78_compress_host")
+    return out.raw[:n.value]

@@ -1,0 +1,739 @@
+// fcx_lz78.hip — the `-c lz78` block codec (FCX8) on gfx950.
+//
+// Reference: my_compress_file_lz78 (my_compress.cpp:3127-3476) over
+// my_LZ78_compress (1832-1899).  Blocks are independent (each call restarts the
+// dictionary), so the device work is block-parallel; inside a block the LZ78
+// parse is a serial trie walk (each phrase's start depends on the previous
+// phrase), so it runs one lane per block over an open-addressed trie in HBM.
+// Everything after the parse is position-parallel:
+//
+//   k78_parse     lane per block: trie walk -> tokens (idx[t], c[t]), N, max idx
+//   k78_mark      token-parallel: bitmap of used indices (3180-3206), char histogram
+//   k78_rank      workgroup per block: popcount prefix of the bitmap -> rank base per
+//                 word, wcnt (mapIdx 3216-3219)
+//   k78_group     token-parallel: rank -> (group = r/256, in-group position r%256),
+//                 group counts (3224-3254)
+//   k78_tree      workgroup per block: the group tree (create_huffman_tree 535-617 on
+//                 G leaves, 3258-3307) and the char tree (987-1066), both as a bitonic
+//                 sort of (weight, symbol) in LDS + the two-queue merge that equals the
+//                 reference's insertion order; code tables; the record layout
+//   k78_scan      record offsets across the shard
+//   k78_tilesum / k78_tilescan / k78_pack
+//                 bit offsets of every 8192-token tile, then each lane packs its 32
+//                 group codes and 32 char codes LSB-first into word staging
+//                 (huffman_encode_idxGroup 2927-3006, huffman_encode_char 849-928)
+//   k78_write     byte-parallel assembly of [u32 len][payload] records
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+
+#include "fcx.h"
+
+namespace fcx78 {
+
+constexpr uint32_t kTileTok = 8192;   // tokens per pack tile (256 lanes x 32)
+constexpr uint32_t kSortCap = 8192;   // bitonic sort capacity (>= max group count 4097)
+
+struct Rec78 {
+    uint32_t N, maxi, wcnt, G;
+    uint32_t Wg, Wc, ts, hlen;   // group words, char words, char tree size, char header bytes
+    uint32_t nbm;                // index bitmap bytes
+    uint32_t o_G, o_tree, o_N, o_gw, o_gpos, o_chdr, o_Wc, o_cw;   // offsets inside the record
+    uint32_t rec;                // 4 + payload
+    uint32_t err;
+};
+
+struct Scratch {
+    uint32_t B, nb, cap_log2, Gmax, tiles;
+    uint64_t *slot;      // nb << cap_log2
+    uint32_t *idx;       // nb * B
+    uint8_t *c;          // nb * B
+    uint32_t *bm;        // nb * bmw
+    uint32_t *rbase;     // nb * bmw
+    uint32_t bmw;
+    uint16_t *grp;       // nb * B
+    uint8_t *gpos;       // nb * B
+    uint32_t *gcnt;      // nb * Gmax
+    uint32_t *chist;     // nb * 256
+    uint32_t *gcode;     // nb * Gmax
+    uint8_t *glen;       // nb * Gmax
+    uint32_t *ccode;     // nb * 256
+    uint8_t *clen;       // nb * 256
+    uint32_t *tree;      // nb * 2 * Gmax (group tree children, u32 pairs)
+    uint32_t *par;       // nb * 2 * Gmax (parent scratch)
+    uint32_t *iw;        // nb * Gmax (internal-node weights scratch)
+    uint8_t *chdr;       // nb * 576
+    uint32_t *tbits;     // nb * tiles * 2
+    uint32_t *gstage;    // nb * (B + 2)
+    uint32_t *cstage;    // nb * (B + 2)
+    Rec78 *rec;          // nb
+    uint64_t *off;       // nb (record offsets in the output)
+    uint64_t *total;     // 1 (running output bytes across batches)
+};
+
+__device__ inline uint64_t trie_hash(uint64_t key) { return (key * 0x9E3779B97F4A7C15ull) >> 17; }
+
+// ---------------------------------------------------------------------------
+// my_LZ78_compress (1832-1899): phrase = longest dictionary prefix + 1 byte; token
+// (prefix index or 0, byte); the phrase enters the dictionary at the next index.  A
+// block whose remainder is a dictionary string ends with (its index, 0) (1858-1863).
+__global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, uint64_t n, Scratch S, uint64_t base_blk) {
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= S.nb) return;
+    const uint64_t off = (base_blk + b) * (uint64_t)S.B;
+    Rec78 &R = S.rec[b];
+    if (off >= n) {
+        R.N = 0;
+        return;
+    }
+    const uint32_t len = (uint32_t)min((uint64_t)S.B, n - off);
+    const uint8_t *src = in + off;
+    uint64_t *slot = S.slot + ((uint64_t)b << S.cap_log2);
+    const uint64_t mask = (1ull << S.cap_log2) - 1;
+    uint32_t *idx = S.idx + (uint64_t)b * S.B;
+    uint8_t *cc = S.c + (uint64_t)b * S.B;
+    uint32_t N = 0, next = 1, pos = 0, maxi = 0;
+    while (pos < len) {
+        uint32_t node = 0;
+        bool put = false;
+        uint64_t h = 0, key = 0;
+        while (pos < len) {
+            key = (((uint64_t)node << 8) | src[pos]) + 1;
+            uint32_t child = 0;
+            for (h = trie_hash(key) & mask;; h = (h + 1) & mask) {
+                const uint64_t s = slot[h];
+                if (s == 0) break;
+                if ((s >> 24) == key) {
+                    child = (uint32_t)(s & 0xFFFFFFu);
+                    break;
+                }
+            }
+            if (!child) {
+                put = true;   // h is the empty slot that ended the probe
+                break;
+            }
+            node = child;
+            pos++;
+        }
+        if (!put) {   // whole remainder found
+            idx[N] = node;
+            cc[N] = 0;
+            N++;
+            maxi = max(maxi, node);
+            break;
+        }
+        slot[h] = (key << 24) | next++;
+        idx[N] = node;
+        cc[N] = src[pos];
+        N++;
+        maxi = max(maxi, node);
+        pos++;
+    }
+    R.N = N;
+    R.maxi = maxi;
+    R.err = 0;
+}
+
+// token-parallel: used-index bitmap + char histogram
+__global__ __launch_bounds__(256) void k78_mark(Scratch S) {
+    __shared__ uint32_t h[256];
+    const uint32_t b = blockIdx.y, tid = threadIdx.x;
+    const uint32_t N = S.rec[b].N;
+    const uint32_t t0 = blockIdx.x * kTileTok;
+    if (t0 >= N) return;
+    h[tid] = 0;
+    __syncthreads();
+    const uint32_t *idx = S.idx + (uint64_t)b * S.B;
+    const uint8_t *cc = S.c + (uint64_t)b * S.B;
+    uint32_t *bm = S.bm + (uint64_t)b * S.bmw;
+    const uint32_t t1 = min(N, t0 + kTileTok);
+    for (uint32_t t = t0 + tid; t < t1; t += 256) {
+        const uint32_t v = idx[t];
+        atomicOr(&bm[v >> 5], 1u << (v & 31));
+        atomicAdd(&h[cc[t]], 1u);
+    }
+    __syncthreads();
+    if (h[tid]) atomicAdd(&S.chist[(uint64_t)b * 256 + tid], h[tid]);
+}
+
+// workgroup per block: exclusive popcount prefix over the bitmap words
+__global__ __launch_bounds__(1024) void k78_rank(Scratch S) {
+    __shared__ uint32_t part[1024];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    Rec78 &R = S.rec[b];
+    if (R.N == 0) return;
+    const uint32_t nw = R.maxi / 32 + 1;
+    const uint32_t per = (nw + 1023) / 1024;
+    const uint32_t w0 = min(nw, tid * per), w1 = min(nw, w0 + per);
+    const uint32_t *bm = S.bm + (uint64_t)b * S.bmw;
+    uint32_t *rb = S.rbase + (uint64_t)b * S.bmw;
+    uint32_t sum = 0;
+    for (uint32_t w = w0; w < w1; w++) sum += __popc(bm[w]);
+    part[tid] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan
+        const uint32_t v = tid >= d ? part[tid - d] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[tid] - sum;
+    for (uint32_t w = w0; w < w1; w++) {
+        rb[w] = run;
+        run += __popc(bm[w]);
+    }
+    if (tid == 1023) {
+        R.wcnt = part[1023];
+        R.G = (part[1023] + 255) / 256;
+        R.nbm = R.maxi / 8 + 1;
+    }
+}
+
+// token-parallel: rank -> group / in-group position, group counts
+__global__ __launch_bounds__(256) void k78_group(Scratch S) {
+    const uint32_t b = blockIdx.y, tid = threadIdx.x;
+    const uint32_t N = S.rec[b].N;
+    const uint32_t t0 = blockIdx.x * kTileTok;
+    if (t0 >= N) return;
+    const uint32_t *idx = S.idx + (uint64_t)b * S.B;
+    const uint32_t *bm = S.bm + (uint64_t)b * S.bmw;
+    const uint32_t *rb = S.rbase + (uint64_t)b * S.bmw;
+    uint16_t *grp = S.grp + (uint64_t)b * S.B;
+    uint8_t *gp = S.gpos + (uint64_t)b * S.B;
+    uint32_t *gc = S.gcnt + (uint64_t)b * S.Gmax;
+    const uint32_t t1 = min(N, t0 + kTileTok);
+    for (uint32_t t = t0 + tid; t < t1; t += 256) {
+        const uint32_t v = idx[t];
+        const uint32_t r = rb[v >> 5] + __popc(bm[v >> 5] & ((1u << (v & 31)) - 1u));
+        grp[t] = (uint16_t)(r >> 8);
+        gp[t] = (uint8_t)(r & 255);
+        atomicAdd(&gc[r >> 8], 1u);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// create_huffman_tree (535-617) on n leaves of weight w[] (zero = absent): leaves
+// stably sorted by weight (sort key (w, symbol)), each merge takes the two list
+// heads (left, right) and re-inserts after every weight <= sum, which is the
+// two-queue merge taking the leaf on a tie.  Internal node k is n + (n - real) + k.
+// lc/rc[k] hold its children (raw node numbers); parent[] is indexed by node.
+// Codes: leaf -> root walk, root edge in bit 0 (869-924, 2947-2992).  Returns real;
+// sets *bad on a code longer than 32 bits.
+__device__ uint32_t wg_tree(uint32_t n, const uint32_t *w, uint64_t *keys /*LDS kSortCap*/, uint32_t *lc,
+                            uint32_t *rc, uint32_t *par, uint32_t *iw, uint32_t *code, uint8_t *clen,
+                            uint32_t *s_real, uint32_t *bad) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    if (tid == 0) *s_real = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < P; i += nt) {
+        const uint32_t wi = i < n ? w[i] : 0u;
+        keys[i] = wi ? ((uint64_t)wi << 32) | i : ~0ull;
+        if (wi) atomicAdd(s_real, 1u);
+    }
+    for (uint32_t i = tid; i < 2 * n; i += nt) par[i] = 0;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < P; i += nt) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = keys[i], c = keys[l];
+                    const bool up = (i & k) == 0;
+                    if ((a > c) == up) {
+                        keys[i] = c;
+                        keys[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const uint32_t real = *s_real;
+    const uint32_t nbase = n + (n - real);
+    if (tid == 0 && real > 1) {
+        uint32_t lh = 0, ih = 0, it = 0;
+        for (uint32_t k = 0; k + 1 < real; k++) {
+            uint32_t pick[2], pw[2];
+            for (int q = 0; q < 2; q++) {
+                const bool leaf = lh < real && (ih == it || (uint32_t)(keys[lh] >> 32) <= iw[ih]);
+                if (leaf) {
+                    pw[q] = (uint32_t)(keys[lh] >> 32);
+                    pick[q] = (uint32_t)keys[lh];
+                    lh++;
+                } else {
+                    pw[q] = iw[ih];
+                    pick[q] = nbase + ih;
+                    ih++;
+                }
+            }
+            const uint32_t node = nbase + k;
+            lc[k] = pick[0];
+            rc[k] = pick[1];
+            par[pick[0]] = node;
+            par[pick[1]] = node;
+            iw[it++] = pw[0] + pw[1];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += nt) {
+        uint32_t bits = 0, depth = 0, cur = i, p = par[i];
+        if (w[i] && real > 1)
+            while (p != 0 && p < 2 * n - 1) {
+                if (depth == 32) {
+                    *bad = 1;
+                    break;
+                }
+                bits = (bits << 1) | (lc[p - nbase] == cur ? 0u : 1u);
+                depth++;
+                cur = p;
+                p = par[p];
+            }
+        code[i] = bits;
+        clen[i] = (uint8_t)depth;
+    }
+    __syncthreads();
+    return real;
+}
+
+__global__ __launch_bounds__(256) void k78_tree(Scratch S) {
+    __shared__ uint64_t keys[kSortCap];
+    __shared__ uint32_t s_real, s_bad;
+    __shared__ uint64_t s_bits[2];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    Rec78 &R = S.rec[b];
+    if (R.N == 0) return;
+    if (tid == 0) {
+        s_bad = 0;
+        s_bits[0] = s_bits[1] = 0;
+    }
+    __syncthreads();
+    const uint32_t G = R.G, Gm = S.Gmax;
+    uint32_t *lc = S.tree + (uint64_t)b * 2 * Gm, *rc = lc + Gm;
+    uint32_t *par = S.par + (uint64_t)b * 2 * Gm, *iw = S.iw + (uint64_t)b * Gm;
+    const uint32_t *gc = S.gcnt + (uint64_t)b * Gm;
+    uint32_t *gcode = S.gcode + (uint64_t)b * Gm;
+    uint8_t *glen = S.glen + (uint64_t)b * Gm;
+    if (G > 1) {
+        wg_tree(G, gc, keys, lc, rc, par, iw, gcode, glen, &s_real, &s_bad);
+        uint64_t part = 0;
+        for (uint32_t g = tid; g < G; g += 256) part += (uint64_t)gc[g] * glen[g];
+        atomicAdd((unsigned long long *)&s_bits[0], (unsigned long long)part);
+    }
+    // char tree (987-1066): the same builder on 256 symbols.  The group tree's parents
+    // and internal weights are spent (its codes and children are stored), so the char
+    // tree borrows that scratch: children in iw[0..511], weights iw[512..767], par[0..511].
+    __syncthreads();
+    const uint32_t *ch = S.chist + (uint64_t)b * 256;
+    uint32_t *ccode = S.ccode + (uint64_t)b * 256;
+    uint8_t *cl = S.clen + (uint64_t)b * 256;
+    uint32_t *xlc = iw, *xrc = iw + 256;
+    const uint32_t real = wg_tree(256, ch, keys, xlc, xrc, par, iw + 512, ccode, cl, &s_real, &s_bad);
+    atomicAdd((unsigned long long *)&s_bits[1], (unsigned long long)ch[tid] * cl[tid]);
+    const uint32_t ts = real > 1 ? real - 1 : 0, hb = (2 * ts + 7) / 8;
+    uint8_t *hdr = S.chdr + (uint64_t)b * 576;
+    // [u8 ts][hb bytes: bit k set = child k of the pairs is internal][ts x (u8 l, u8 r)]
+    for (uint32_t q = tid; q < hb; q += 256) {
+        uint32_t v = 0;
+        for (uint32_t k = 8 * q; k < min(8 * q + 8, 2 * ts); k++)
+            if (((k & 1) ? xrc[k >> 1] : xlc[k >> 1]) >= 256) v |= 1u << (k & 7);
+        hdr[1 + q] = (uint8_t)v;
+    }
+    for (uint32_t j = tid; j < ts; j += 256) {
+        const uint32_t l = xlc[j], r = xrc[j];
+        hdr[1 + hb + 2 * j] = (uint8_t)(l >= 256 ? l - 256 : l);
+        hdr[1 + hb + 2 * j + 1] = (uint8_t)(r >= 256 ? r - 256 : r);
+    }
+    if (tid == 0) hdr[0] = (uint8_t)ts;
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t N = R.N;
+        R.Wg = G > 1 ? (uint32_t)((s_bits[0] + 31) / 32) : 0u;
+        R.Wc = (uint32_t)((s_bits[1] + 31) / 32);
+        R.ts = ts;
+        R.hlen = 1 + hb + 2 * ts;
+        uint32_t o = 4 + 4 + R.nbm;   // [u32 len][u32 wcnt][bitmap]
+        R.o_G = o;
+        o += 4;
+        R.o_tree = o;
+        if (G > 1) {
+            o += 8 * (G - 1);
+            R.o_N = o;
+            o += 8;   // N, Wg
+            R.o_gw = o;
+            o += 4 * R.Wg;
+        } else {
+            R.o_N = o;
+            o += 4;
+            R.o_gw = o;
+        }
+        R.o_gpos = o;
+        o += N;
+        R.o_chdr = o;
+        o += R.hlen;
+        R.o_Wc = o;
+        o += 4;
+        R.o_cw = o;
+        o += 4 * R.Wc;
+        R.rec = o;
+        R.err = s_bad;
+    }
+}
+
+// record offsets across the shard (one workgroup; serial chunks + LDS scan)
+__global__ __launch_bounds__(1024) void k78_scan(Scratch S, uint64_t cap, uint32_t *err) {
+    __shared__ uint64_t part[1024];
+    const uint32_t tid = threadIdx.x, nb = S.nb;
+    const uint32_t per = (nb + 1023) / 1024, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+    uint64_t sum = 0;
+    for (uint32_t b = b0; b < b1; b++) {
+        const Rec78 &R = S.rec[b];
+        if (R.N) sum += R.rec;
+        if (R.N && R.err) atomicOr(err, 1u);
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = tid >= d ? part[tid - d] : 0ull;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    const uint64_t base = *S.total;
+    uint64_t run = base + part[tid] - sum;
+    for (uint32_t b = b0; b < b1; b++) {
+        S.off[b] = run;
+        if (S.rec[b].N) run += S.rec[b].rec;
+    }
+    __syncthreads();
+    if (tid == 1023) {
+        *S.total = base + part[1023];
+        if (base + part[1023] > cap) atomicOr(err, 2u);
+    }
+}
+
+__device__ inline void tok_codes(const Scratch &S, uint32_t b, uint32_t t, uint32_t G, uint32_t &gcw, uint32_t &glw,
+                                 uint32_t &ccw, uint32_t &clw) {
+    const uint8_t sym = S.c[(uint64_t)b * S.B + t];
+    ccw = S.ccode[(uint64_t)b * 256 + sym];
+    clw = S.clen[(uint64_t)b * 256 + sym];
+    if (G > 1) {
+        const uint32_t g = S.grp[(uint64_t)b * S.B + t];
+        gcw = S.gcode[(uint64_t)b * S.Gmax + g];
+        glw = S.glen[(uint64_t)b * S.Gmax + g];
+    } else {
+        gcw = glw = 0;
+    }
+}
+
+// bits of each tile (both streams)
+__global__ __launch_bounds__(256) void k78_tilesum(Scratch S) {
+    __shared__ uint32_t sg, sc;
+    const uint32_t b = blockIdx.y, tid = threadIdx.x;
+    const Rec78 &R = S.rec[b];
+    const uint32_t t0 = blockIdx.x * kTileTok;
+    if (t0 >= R.N) return;
+    if (tid == 0) sg = sc = 0;
+    __syncthreads();
+    uint32_t a = 0, c = 0;
+    for (uint32_t t = t0 + tid * 32; t < min(R.N, t0 + tid * 32 + 32); t++) {
+        uint32_t gcw, glw, ccw, clw;
+        tok_codes(S, b, t, R.G, gcw, glw, ccw, clw);
+        a += glw;
+        c += clw;
+    }
+    atomicAdd(&sg, a);
+    atomicAdd(&sc, c);
+    __syncthreads();
+    if (tid == 0) {
+        S.tbits[((uint64_t)b * S.tiles + blockIdx.x) * 2] = sg;
+        S.tbits[((uint64_t)b * S.tiles + blockIdx.x) * 2 + 1] = sc;
+    }
+}
+
+__global__ __launch_bounds__(64) void k78_tilescan(Scratch S) {
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= S.nb || S.rec[b].N == 0) return;
+    const uint32_t nt = (S.rec[b].N + kTileTok - 1) / kTileTok;
+    uint32_t a = 0, c = 0;
+    uint32_t *tb = S.tbits + (uint64_t)b * S.tiles * 2;
+    for (uint32_t i = 0; i < nt; i++) {
+        const uint32_t x = tb[2 * i], y = tb[2 * i + 1];
+        tb[2 * i] = a;
+        tb[2 * i + 1] = c;
+        a += x;
+        c += y;
+    }
+}
+
+__device__ inline void put_bits(uint32_t *w, uint32_t off, uint32_t code, uint32_t len) {
+    if (!len) return;
+    const uint64_t v = (uint64_t)code << (off & 31);
+    atomicOr(&w[off >> 5], (uint32_t)v);
+    if ((off & 31) + len > 32) atomicOr(&w[(off >> 5) + 1], (uint32_t)(v >> 32));
+}
+
+__global__ __launch_bounds__(256) void k78_pack(Scratch S) {
+    __shared__ uint32_t pg[256], pc[256];
+    const uint32_t b = blockIdx.y, tid = threadIdx.x;
+    const Rec78 &R = S.rec[b];
+    const uint32_t t0 = blockIdx.x * kTileTok;
+    if (t0 >= R.N) return;
+    const uint32_t i0 = t0 + tid * 32, i1 = min(R.N, i0 + 32);
+    uint32_t a = 0, c = 0;
+    for (uint32_t t = i0; t < i1; t++) {
+        uint32_t gcw, glw, ccw, clw;
+        tok_codes(S, b, t, R.G, gcw, glw, ccw, clw);
+        a += glw;
+        c += clw;
+    }
+    pg[tid] = a;
+    pc[tid] = c;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        const uint32_t x = tid >= d ? pg[tid - d] : 0u, y = tid >= d ? pc[tid - d] : 0u;
+        __syncthreads();
+        pg[tid] += x;
+        pc[tid] += y;
+        __syncthreads();
+    }
+    const uint32_t *tb = S.tbits + ((uint64_t)b * S.tiles + blockIdx.x) * 2;
+    uint32_t og = tb[0] + pg[tid] - a, oc = tb[1] + pc[tid] - c;
+    uint32_t *gw = S.gstage + (uint64_t)b * (S.B + 2), *cw = S.cstage + (uint64_t)b * (S.B + 2);
+    for (uint32_t t = i0; t < i1; t++) {
+        uint32_t gcw, glw, ccw, clw;
+        tok_codes(S, b, t, R.G, gcw, glw, ccw, clw);
+        put_bits(gw, og, gcw, glw);
+        put_bits(cw, oc, ccw, clw);
+        og += glw;
+        oc += clw;
+    }
+}
+
+__device__ inline uint8_t u32_byte(uint32_t v, uint32_t k) { return (uint8_t)(v >> (8 * k)); }
+
+// byte-parallel record assembly (layout: my_compress_file_lz78 3127-3476)
+__global__ __launch_bounds__(256) void k78_write(Scratch S, uint8_t *__restrict__ out, const uint32_t *err) {
+    const uint32_t b = blockIdx.y;
+    const Rec78 &R = S.rec[b];
+    if (R.N == 0 || *err) return;
+    uint8_t *o = out + S.off[b];
+    const uint32_t rec = R.rec;
+    const uint8_t *bmb = (const uint8_t *)(S.bm + (uint64_t)b * S.bmw);
+    const uint32_t *lc = S.tree + (uint64_t)b * 2 * S.Gmax, *rc = lc + S.Gmax;
+    const uint8_t *gw = (const uint8_t *)(S.gstage + (uint64_t)b * (S.B + 2));
+    const uint8_t *cw = (const uint8_t *)(S.cstage + (uint64_t)b * (S.B + 2));
+    const uint8_t *gp = S.gpos + (uint64_t)b * S.B;
+    const uint8_t *hdr = S.chdr + (uint64_t)b * 576;
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < rec; p += gridDim.x * 256) {
+        uint8_t v;
+        if (p < 4) v = u32_byte(rec - 4, p);
+        else if (p < 8) v = u32_byte(R.wcnt, p - 4);
+        else if (p < R.o_G) v = bmb[p - 8];
+        else if (p < R.o_tree) v = u32_byte(R.G, p - R.o_G);
+        else if (p < R.o_N) {
+            const uint32_t q = p - R.o_tree, j = q / 8, k = q % 8;
+            v = u32_byte(k < 4 ? lc[j] : rc[j], k & 3);
+        } else if (R.G > 1 && p < R.o_N + 4) v = u32_byte(R.N, p - R.o_N);
+        else if (R.G > 1 && p < R.o_gw) v = u32_byte(R.Wg, p - R.o_N - 4);
+        else if (R.G <= 1 && p < R.o_gw) v = u32_byte(R.N, p - R.o_N);
+        else if (p < R.o_gpos) v = gw[p - R.o_gw];
+        else if (p < R.o_chdr) v = gp[p - R.o_gpos];
+        else if (p < R.o_Wc) v = hdr[p - R.o_chdr];
+        else if (p < R.o_cw) v = u32_byte(R.Wc, p - R.o_Wc);
+        else v = cw[p - R.o_cw];
+        o[p] = v;
+    }
+}
+
+}  // namespace fcx78
+
+using namespace fcx78;
+
+namespace fcx {
+void set_last_error(const std::string &m);   // fcx_capi.hip (fcx_last_error)
+}
+namespace {
+int fail78(int code, const std::string &m) {
+    fcx::set_last_error(m);
+    return code;
+}
+#define H78(expr)                                                                               \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess) return fail78(FCX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Alloc78 {
+    Scratch S{};
+    void *mem = nullptr;
+    ~Alloc78() {
+        if (mem) (void)hipFree(mem);
+    }
+};
+
+int setup(Alloc78 &A, uint32_t B, uint32_t nb) {
+    Scratch &S = A.S;
+    S.B = B;
+    S.nb = nb;
+    S.cap_log2 = 10;
+    while ((1ull << S.cap_log2) < 2ull * B + 2) S.cap_log2++;
+    S.Gmax = B / 256 + 2;
+    if (S.Gmax < 1024) S.Gmax = 1024;   // the char tree borrows iw[0..511]; parents need 2*256
+    S.tiles = (B + 1 + kTileTok - 1) / kTileTok;
+    S.bmw = B / 32 + 2;
+    const uint64_t nbl = nb;
+    uint64_t sz[] = {
+        (nbl << S.cap_log2) * 8, nbl * B * 4, nbl * B, nbl * S.bmw * 4, nbl * S.bmw * 4, nbl * B * 2, nbl * B,
+        nbl * S.Gmax * 4, nbl * 256 * 4, nbl * S.Gmax * 4, nbl * S.Gmax, nbl * 256 * 4, nbl * 256,
+        nbl * 2 * S.Gmax * 4, nbl * 2 * S.Gmax * 4, nbl * S.Gmax * 4, nbl * 576, nbl * S.tiles * 8,
+        nbl * (B + 2) * 4, nbl * (B + 2) * 4, nbl * sizeof(Rec78), nbl * 8, 8};
+    constexpr int K = sizeof(sz) / sizeof(sz[0]);
+    uint64_t offs[K], tot = 0;
+    for (int i = 0; i < K; i++) {
+        offs[i] = tot;
+        tot += (sz[i] + 255) & ~255ull;
+    }
+    H78(hipMalloc(&A.mem, tot));
+    char *m = (char *)A.mem;
+    S.slot = (uint64_t *)(m + offs[0]);
+    S.idx = (uint32_t *)(m + offs[1]);
+    S.c = (uint8_t *)(m + offs[2]);
+    S.bm = (uint32_t *)(m + offs[3]);
+    S.rbase = (uint32_t *)(m + offs[4]);
+    S.grp = (uint16_t *)(m + offs[5]);
+    S.gpos = (uint8_t *)(m + offs[6]);
+    S.gcnt = (uint32_t *)(m + offs[7]);
+    S.chist = (uint32_t *)(m + offs[8]);
+    S.gcode = (uint32_t *)(m + offs[9]);
+    S.glen = (uint8_t *)(m + offs[10]);
+    S.ccode = (uint32_t *)(m + offs[11]);
+    S.clen = (uint8_t *)(m + offs[12]);
+    S.tree = (uint32_t *)(m + offs[13]);
+    S.par = (uint32_t *)(m + offs[14]);
+    S.iw = (uint32_t *)(m + offs[15]);
+    S.chdr = (uint8_t *)(m + offs[16]);
+    S.tbits = (uint32_t *)(m + offs[17]);
+    S.gstage = (uint32_t *)(m + offs[18]);
+    S.cstage = (uint32_t *)(m + offs[19]);
+    S.rec = (Rec78 *)(m + offs[20]);
+    S.off = (uint64_t *)(m + offs[21]);
+    S.total = (uint64_t *)(m + offs[22]);
+    return FCX_OK;
+}
+
+// scratch footprint per block is ~50 B per input byte (trie 32 B): batches keep it bounded
+constexpr uint64_t kBatchBytes = 256ull << 20;
+}  // namespace
+
+extern "C" {
+
+int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_bytes, uint8_t *d_out, uint64_t cap,
+                            uint64_t *out_len, void *stream) {
+    if (!d_out || !out_len || (n && !d_in)) return fail78(FCX_ERR_ARG, "fcx_lz78_compress_shard: NULL argument");
+    if (block_bytes == 0 || block_bytes > FCX_MAX_BLOCK_BYTES)
+        return fail78(FCX_ERR_ARG, "fcx_lz78_compress_shard: block_bytes must be in [1, 1 MiB]");
+    *out_len = 0;
+    if (n == 0) return FCX_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const uint64_t nblk = (n + block_bytes - 1) / block_bytes;
+    const uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nblk, kBatchBytes / block_bytes));
+    Alloc78 A;
+    if (int rc = setup(A, block_bytes, batch)) return rc;
+    Scratch S = A.S;
+    uint32_t *d_err = nullptr;
+    H78(hipMalloc(&d_err, 4));
+    struct ErrFree {
+        uint32_t *p;
+        ~ErrFree() { (void)hipFree(p); }
+    } ef{d_err};
+    H78(hipMemsetAsync(d_err, 0, 4, st));
+    H78(hipMemsetAsync(S.total, 0, 8, st));
+    for (uint64_t b0 = 0; b0 < nblk; b0 += batch) {
+        S.nb = (uint32_t)std::min<uint64_t>(batch, nblk - b0);
+        const uint32_t nb = S.nb;
+        H78(hipMemsetAsync(S.slot, 0, ((uint64_t)nb << S.cap_log2) * 8, st));
+        H78(hipMemsetAsync(S.bm, 0, (uint64_t)nb * S.bmw * 4, st));
+        H78(hipMemsetAsync(S.gcnt, 0, (uint64_t)nb * S.Gmax * 4, st));
+        H78(hipMemsetAsync(S.chist, 0, (uint64_t)nb * 256 * 4, st));
+        H78(hipMemsetAsync(S.gstage, 0, (uint64_t)nb * (S.B + 2) * 4, st));
+        H78(hipMemsetAsync(S.cstage, 0, (uint64_t)nb * (S.B + 2) * 4, st));
+        const dim3 tok_grid(S.tiles, nb);
+        k78_parse<<<(nb + 63) / 64, 64, 0, st>>>(d_in, n, S, b0);
+        k78_mark<<<tok_grid, 256, 0, st>>>(S);
+        k78_rank<<<nb, 1024, 0, st>>>(S);
+        k78_group<<<tok_grid, 256, 0, st>>>(S);
+        k78_tree<<<nb, 256, 0, st>>>(S);
+        k78_scan<<<1, 1024, 0, st>>>(S, cap, d_err);
+        k78_tilesum<<<tok_grid, 256, 0, st>>>(S);
+        k78_tilescan<<<(nb + 63) / 64, 64, 0, st>>>(S);
+        k78_pack<<<tok_grid, 256, 0, st>>>(S);
+        k78_write<<<dim3(64, nb), 256, 0, st>>>(S, d_out, d_err);
+        H78(hipGetLastError());
+    }
+    uint32_t herr = 0;
+    uint64_t total = 0;
+    H78(hipMemcpyAsync(&herr, d_err, 4, hipMemcpyDeviceToHost, st));
+    H78(hipMemcpyAsync(&total, S.total, 8, hipMemcpyDeviceToHost, st));
+    H78(hipStreamSynchronize(st));
+    if (herr & 2) return fail78(FCX_ERR_CAPACITY, "fcx_lz78_compress_shard: output capacity exceeded");
+    if (herr & 1) return fail78(FCX_ERR_INTERNAL, "fcx_lz78_compress_shard: Huffman code longer than 32 bits");
+    *out_len = total;
+    return FCX_OK;
+}
+
+int fcx_lz78_compress_host(const uint8_t *in, uint64_t n, uint32_t block_bytes, uint8_t *out, uint64_t cap,
+                           uint64_t *out_len) {
+    if (!in || !out || !out_len) return fail78(FCX_ERR_ARG, "fcx_lz78_compress_host: NULL argument");
+    if (cap < FCX_HEADER_BYTES) return fail78(FCX_ERR_CAPACITY, "fcx_lz78_compress_host: capacity below the header");
+    if (block_bytes == 0 || block_bytes > FCX_MAX_BLOCK_BYTES)
+        return fail78(FCX_ERR_ARG, "fcx_lz78_compress_host: block_bytes must be in [1, 1 MiB]");
+    const uint64_t nblk = (n + block_bytes - 1) / block_bytes;
+    memcpy(out, "FCX8", 4);   // stCmpFileHead (101-109) with the lz78 tag (4079-4086)
+    const uint32_t tot32 = (uint32_t)n;
+    const uint16_t nb16 = (uint16_t)nblk;
+    memcpy(out + 4, &tot32, 4);
+    memcpy(out + 8, &nb16, 2);
+    *out_len = FCX_HEADER_BYTES;
+    if (n == 0) return FCX_OK;
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    H78(hipMalloc(&d_in, n));
+    struct F {
+        uint8_t **a, **b;
+        ~F() {
+            if (*a) (void)hipFree(*a);
+            if (*b) (void)hipFree(*b);
+        }
+    } f{&d_in, &d_out};
+    const uint64_t dcap = cap - FCX_HEADER_BYTES;
+    H78(hipMalloc(&d_out, dcap ? dcap : 16));
+    H78(hipMemcpy(d_in, in, n, hipMemcpyHostToDevice));
+    uint64_t len = 0;
+    if (int rc = fcx_lz78_compress_shard(d_in, n, block_bytes, d_out, dcap, &len, nullptr)) return rc;
+    H78(hipMemcpy(out + FCX_HEADER_BYTES, d_out, len, hipMemcpyDeviceToHost));
+    *out_len = FCX_HEADER_BYTES + len;
+    return FCX_OK;
+}
+
+uint32_t fcx_lz78_compress_block(const void *in, uint32_t len, uint8_t *out) {
+    if (!in || !out || len == 0 || len > FCX_MAX_BLOCK_BYTES) return 0;
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    const uint64_t cap = 10ull * len + 4096;
+    if (hipMalloc(&d_in, len) != hipSuccess) return 0;
+    if (hipMalloc(&d_out, cap) != hipSuccess) {
+        (void)hipFree(d_in);
+        return 0;
+    }
+    uint64_t got = 0;
+    uint32_t ret = 0;
+    if (hipMemcpy(d_in, in, len, hipMemcpyHostToDevice) == hipSuccess &&
+        fcx_lz78_compress_shard(d_in, len, len, d_out, cap, &got, nullptr) == FCX_OK && got >= 4 &&
+        hipMemcpy(out, d_out + 4, got - 4, hipMemcpyDeviceToHost) == hipSuccess)
+        ret = (uint32_t)(got - 4);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return ret;
+}
+
+}  // extern "C"

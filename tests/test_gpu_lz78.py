@@ -1,0 +1,65 @@
+"""GPU parity of the `-c lz78` codec (fcx_lz78.hip, through the C ABI) against the
+LZ78 oracle (oracle/lz78_oracle.c, itself pinned by tests/test_lz78.py against the
+reference compiled in place and tests/golden/golden_lz78.json).  Integer/byte
+work: bit-exact.  Reference: my_compress_file_lz78 my_compress.cpp:3127-3476,
+main() -c lz78 4073-4136."""
+import hashlib
+import json
+import os
+
+import pytest
+
+import inputs
+import my_compress_amd as mc
+import oracle
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def test_golden_files():
+    with open(os.path.join(HERE, "golden", "golden_lz78.json")) as f:
+        g = json.load(f)
+    for rec in g["cases"]:
+        data = inputs.make(rec)
+        out = mc.compress_lz78(data, rec["block"])
+        assert len(out) == rec["out_bytes"], rec["name"]
+        assert sha(out) == rec["out_sha256"], rec["name"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 255, 256, 4097, 65536, 200003])
+def test_block_vs_oracle(n):
+    data = inputs.mosaic(300 + n, n)
+    assert mc.my_compress_file_lz78(data) == oracle.lz78_compress_block(data)
+
+
+@pytest.mark.parametrize("kind", ["rand", "text", "zeros", "runs"])
+def test_file_vs_oracle(kind):
+    n, block = (3 << 20) + 12345, 1 << 20
+    data = inputs.generate(kind, 7, n)
+    assert mc.compress_lz78(data, block) == oracle.lz78_compress_file(data, block)
+
+
+def test_small_blocks_many_batches_vs_oracle():
+    # 64 KiB blocks: several hundred records, last one ragged
+    data = inputs.mosaic(77, (20 << 20) + 999)
+    assert mc.compress_lz78(data, 1 << 16) == oracle.lz78_compress_file(data, 1 << 16)
+
+
+def test_edge_inputs():
+    for data in [b"a", b"aaaa", b"\0\0\0", bytes(range(256)), bytes(100000), b"ab" * 50000]:
+        assert mc.compress_lz78(data, 1 << 20) == oracle.lz78_compress_file(data, 1 << 20)
+    assert mc.compress_lz78(b"", 1 << 20) == oracle.lz78_compress_file(b"", 1 << 20)
+
+
+def test_capacity_error():
+    data = inputs.generate("rand", 1, 100000)
+    import ctypes
+    out = ctypes.create_string_buffer(1000)
+    n = ctypes.c_uint64()
+    rc = mc.lib().fcx_lz78_compress_host(data, len(data), 1 << 20, out, 1000, ctypes.byref(n))
+    assert rc == -2
