@@ -176,6 +176,13 @@ int fcx_lz78_compress_host(const uint8_t *in, uint64_t n, uint32_t block_bytes, 
                            uint64_t *out_len);
 /* one block: payload bytes (no length prefix), 0 on NULL / error; out >= 10*len + 4096. */
 uint32_t fcx_lz78_compress_block(const void *in, uint32_t len, uint8_t *out);
+/*   fcx_lz78_decompress_block <- my_decompress_file_lz78(void*, uInt32, FILE*)       :3478 (called at :4189)
+ *   fcx_lz78_decompress_host  <- the whole decompress mode of main() for FCX8        :4137-4204
+ * GPU decoder, one lane per record; keeps the reference's quirks (a block whose decoded
+ * bytes end in 0x00 loses that byte, 3701-3703; a one-symbol char stream decodes as
+ * zeros).  decompress_block returns decoded bytes or a negative FCX_ERR_*. */
+int64_t fcx_lz78_decompress_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap);
+int fcx_lz78_decompress_host(const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t cap, uint64_t *out_len);
 
 const char *fcx_last_error(void);
 const char *fcx_version(void);

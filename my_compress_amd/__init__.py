@@ -95,6 +95,10 @@ def lib():
                                          ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_lz78_compress_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, c_u8p]
     L.fcx_lz78_compress_block.restype = ctypes.c_uint32
+    L.fcx_lz78_decompress_block.argtypes = [c_u8p, ctypes.c_uint32, c_u8p, ctypes.c_uint64]
+    L.fcx_lz78_decompress_block.restype = ctypes.c_int64
+    L.fcx_lz78_decompress_host.argtypes = [c_u8p, ctypes.c_uint64, c_u8p, ctypes.c_uint64,
+                                           ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_last_error.restype = ctypes.c_char_p
     L.fcx_version.restype = ctypes.c_char_p
     _lib = L
@@ -352,4 +356,24 @@ def compress_lz78(data: bytes, block_bytes: int = BLOCK_BYTES) -> bytes:
     n = ctypes.c_uint64()
     _check(lib().fcx_lz78_compress_host(data, len(data), block_bytes, out, cap, ctypes.byref(n)),
            "fcx_lz78_compress_host")
+    return out.raw[:n.value]
+
+
+def my_decompress_file_lz78(payload: bytes, cap: int = BLOCK_BYTES + 8) -> bytes:
+    """one payload -> block bytes on the GPU (reference decoder semantics, :3478)"""
+    out = ctypes.create_string_buffer(max(cap, 1))
+    got = lib().fcx_lz78_decompress_block(payload, len(payload), out, cap)
+    if got < 0:
+        raise FcxError(f"fcx_lz78_decompress_block failed ({got}): {lib().fcx_last_error().decode(errors='replace')}")
+    return out.raw[:got]
+
+
+def decompress_lz78(blob: bytes, cap: int = None) -> bytes:
+    """whole FCX8 file -> bytes on the GPU (main() decompress mode, :4137-4204)"""
+    if cap is None:
+        nb = struct.unpack_from("<H", blob, 8)[0] if len(blob) >= HEADER_BYTES else 0
+        cap = nb * (BLOCK_BYTES + 8)
+    out = ctypes.create_string_buffer(max(cap, 1))
+    n = ctypes.c_uint64()
+    _check(lib().fcx_lz78_decompress_host(blob, len(blob), out, cap, ctypes.byref(n)), "fcx_lz78_decompress_host")
     return out.raw[:n.value]

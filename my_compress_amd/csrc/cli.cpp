@@ -9,8 +9,9 @@
 // fcx_decompress_stream: file reads and writes overlap the device work); without
 // a HIP device, compress fails and decompress uses the host decoder.  Superset:
 // -b/--block BYTES (<= 1 MiB; the reference fixes 1 MiB, BLOCK_BYTES :113) and
-// -d/--device N.  `-c lz78` (the LZ78 codec) is outside
-// this build's scope and is rejected.
+// -d/--device N.  `-c lz78` runs the LZ78 codec (FCX8) on the GPU: 256 MiB shards
+// through fcx_lz78_compress_host / fcx_lz78_decompress_host (whole files in host
+// memory for decompress).
 #include <getopt.h>
 
 #include <chrono>
@@ -19,6 +20,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <hip/hip_runtime.h>
 
 #include "fcx.h"
 
@@ -106,6 +109,62 @@ static int decompress_host(FILE *fin, FILE *fout, uint32_t total, uint16_t nbloc
     return report(got_total, total);
 }
 
+// FCX8 (-c lz78): 256 MiB shards of whole blocks, each through the GPU codec
+static int compress_lz78(FILE *fin, FILE *fout, uint32_t block) {
+    const uint64_t shard = (256ull << 20) / block * block;
+    std::vector<uint8_t> buf(shard), out;
+    uint8_t hdr[FCX_HEADER_BYTES];
+    memcpy(hdr, "FCX8", 4);
+    memset(hdr + 4, 0, 6);
+    fwrite(hdr, 1, sizeof(hdr), fout);   // placeholder, rewritten at the end (4079-4086)
+    uint64_t total_in = 0, total_out = 0, nblocks = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const size_t n = fread(buf.data(), 1, buf.size(), fin);
+        if (n == 0) break;
+        out.resize(FCX_HEADER_BYTES + 10 * n + 4096 * (n / block + 1));
+        uint64_t got = 0;
+        if (fcx_lz78_compress_host(buf.data(), n, block, out.data(), out.size(), &got)) {
+            fprintf(stderr, "fcx: %s\n", fcx_last_error());
+            return -1;
+        }
+        fwrite(out.data() + FCX_HEADER_BYTES, 1, got - FCX_HEADER_BYTES, fout);
+        total_in += n;
+        total_out += got - FCX_HEADER_BYTES;
+        nblocks += (n + block - 1) / block;
+    }
+    const uint32_t t32 = (uint32_t)total_in;
+    const uint16_t nb16 = (uint16_t)nblocks;
+    memcpy(hdr + 4, &t32, 4);
+    memcpy(hdr + 8, &nb16, 2);
+    fseek(fout, 0, SEEK_SET);
+    fwrite(hdr, 1, sizeof(hdr), fout);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    printf("<Final>: LZ78 totalBytes = %llu, compress total bytes=%llu, compress rate: %.2f%%\n",
+           (unsigned long long)total_in, (unsigned long long)total_out,
+           total_in ? 100.0 * (double)total_out / (double)total_in : 0.0);
+    printf("[***TIME***]  All block compress spend %.0f ms!!!\n", ms);
+    return 0;
+}
+
+static int decompress_lz78(FILE *fin, FILE *fout, uint32_t total) {
+    rewind(fin);
+    std::vector<uint8_t> blob;
+    uint8_t tmp[1 << 16];
+    size_t n;
+    while ((n = fread(tmp, 1, sizeof(tmp), fin)) > 0) blob.insert(blob.end(), tmp, tmp + n);
+    uint16_t nblocks;
+    memcpy(&nblocks, blob.data() + 8, 2);
+    std::vector<uint8_t> out((uint64_t)nblocks * (FCX_MAX_BLOCK_BYTES + 8) + 1);
+    uint64_t got = 0;
+    if (fcx_lz78_decompress_host(blob.data(), blob.size(), out.data(), out.size(), &got)) {
+        fprintf(stderr, "fcx: %s\n", fcx_last_error());
+        return -1;
+    }
+    fwrite(out.data(), 1, (size_t)got, fout);
+    return report(got, total);
+}
+
 static int do_decompress(FILE *fin, FILE *fout, int device) {
     uint8_t hdr[FCX_HEADER_BYTES];
     if (fread(hdr, 1, sizeof(hdr), fin) != sizeof(hdr)) {
@@ -119,10 +178,7 @@ static int do_decompress(FILE *fin, FILE *fout, int device) {
         fprintf(stderr, "This file is not support to decompress!!!!\n");
         return -1;
     }
-    if (kind != '7') {
-        fprintf(stderr, "LZ78 streams are outside this build's scope\n");
-        return -1;
-    }
+    if (kind != '7') return decompress_lz78(fin, fout, total);
     fcx_dctx *d = nullptr;
     if (fcx_dctx_create(&d, device) != FCX_OK) {
         fprintf(stderr, "fcx: %s; decoding on the host\n", fcx_last_error());
@@ -168,10 +224,6 @@ int main(int argc, char **argv) {
         }
     }
     if (file_in.empty()) return usage();
-    if (compress && !lz77) {
-        fprintf(stderr, "-c lz78: the LZ78 codec is outside this build's scope\n");
-        return -1;
-    }
     if (block == 0 || block > FCX_MAX_BLOCK_BYTES) {
         fprintf(stderr, "block size must be in [1, %u]\n", FCX_MAX_BLOCK_BYTES);
         return -1;
@@ -180,7 +232,13 @@ int main(int argc, char **argv) {
     if (!fin) { printf("open: %s Fail!!\n", file_in.c_str()); return -1; }
     FILE *fout = fopen(file_out.c_str(), "wb");
     if (!fout) { printf("open: %s Fail!!\n", file_out.c_str()); fclose(fin); return -1; }
-    const int r = compress ? do_compress(fin, fout, block, device) : do_decompress(fin, fout, device);
+    if (!compress) (void)hipSetDevice(device);   // the FCX8 decoder runs on the current device
+    if (compress && !lz77 && hipSetDevice(device) != hipSuccess) {
+        fprintf(stderr, "fcx: no HIP device %d\n", device);
+        return -1;
+    }
+    const int r = compress ? (lz77 ? do_compress(fin, fout, block, device) : compress_lz78(fin, fout, block))
+                           : do_decompress(fin, fout, device);
     fclose(fin);
     fclose(fout);
     return r;

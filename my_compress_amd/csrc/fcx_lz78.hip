@@ -27,6 +27,8 @@
 
 #include <cstring>
 #include <string>
+#include <vector>
+#include <algorithm>
 
 #include "fcx.h"
 
@@ -734,6 +736,284 @@ uint32_t fcx_lz78_compress_block(const void *in, uint32_t len, uint8_t *out) {
     (void)hipFree(d_in);
     (void)hipFree(d_out);
     return ret;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Decoder: my_decompress_file_lz78 (my_compress.cpp:3478-3710).  Every phrase copies
+// an earlier phrase of the same block, so a block decodes serially; records are
+// independent, so one lane decodes one record (group codes, char codes, in-group
+// positions and phrase copies in a single pass), and a byte-parallel kernel packs
+// the decoded blocks densely.
+namespace fcx78 {
+
+struct Dec78 {
+    uint32_t B;             // per-record output capacity (FCX_MAX_BLOCK_BYTES + 8)
+    uint32_t nb;
+    const uint8_t *in;      // the records' payloads
+    const uint64_t *roff;   // payload offset per record
+    const uint32_t *rlen;   // payload bytes per record
+    uint8_t *out;           // nb * B decoded bytes
+    uint32_t *pindex;       // nb * (B + 2)
+    uint32_t *pstart;       // nb * B
+    uint32_t *plen;         // nb * B
+    uint32_t *lc;           // nb * 2 * Gmax
+    uint32_t Gmax;
+    uint64_t *dlen;         // decoded bytes per record, or ~0 = malformed
+};
+
+__device__ inline uint32_t rd32(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+struct BitRd {   // LSB-first u32 words, W of them
+    const uint8_t *w;
+    uint32_t W, i, cur, left;
+    __device__ int next() {   // -1 when exhausted
+        if (left == 0) {
+            if (i >= W) return -1;
+            cur = rd32(w + 4ull * i++);
+            left = 32;
+        }
+        const int b = cur & 1;
+        cur >>= 1;
+        left--;
+        return b;
+    }
+};
+
+__device__ int64_t dec_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap, uint32_t *pindex,
+                             uint32_t *pstart, uint32_t *plen, uint32_t *glc, uint32_t Gmax) {
+    const uint8_t *q = in, *end = in + len;
+    if (len < 4) return -1;
+    const uint32_t wcnt = rd32(q);
+    q += 4;
+    if (wcnt == 0 || wcnt > cap + 2) return -1;   // the reference reads pIndex[-1] (3502)
+    {   // 3494-3500: indices of the set bits, ascending
+        uint32_t i = 0;
+        for (uint64_t v = 0; i < wcnt; v++) {
+            if ((uint64_t)(end - q) <= (v >> 3)) return -1;
+            if ((q[v >> 3] >> (v & 7)) & 1) pindex[i++] = (uint32_t)v;
+        }
+    }
+    q += pindex[wcnt - 1] / 8 + 1;
+    if (end - q < 4) return -1;
+    const uint32_t G = rd32(q);
+    q += 4;
+    uint32_t N;
+    BitRd gr{nullptr, 0, 0, 0, 0};
+    uint32_t *grc = glc + Gmax;
+    if (G > 1) {
+        if (G > Gmax || (uint64_t)(end - q) < 8ull * (G - 1) + 8) return -1;
+        for (uint32_t j = 0; j + 1 < G; j++) {
+            glc[j] = rd32(q);
+            grc[j] = rd32(q + 4);
+            q += 8;
+        }
+        N = rd32(q);
+        const uint32_t W = rd32(q + 4);
+        q += 8;
+        if ((uint64_t)(end - q) < 4ull * W) return -1;
+        gr = BitRd{q, W, 0, 0, 0};
+        q += 4ull * W;
+    } else {
+        if (end - q < 4) return -1;
+        N = rd32(q);
+        q += 4;
+    }
+    if ((uint64_t)(end - q) < N || N > cap) return -1;
+    const uint8_t *gpos = q;
+    q += N;
+    // char sub-stream header (huffman_decode_char 930-984, my_huffman_decode_char 1107-1187)
+    const uint32_t avail = (uint32_t)(end - q);
+    if (avail < 1) return -1;
+    const uint32_t ts = q[0], nbm = (2 * ts + 7) / 8, hdr = 1 + nbm + 2 * ts;
+    if (avail < hdr + 4) return -1;
+    const uint8_t *bm = q + 1, *pairs = q + 1 + nbm;
+    const uint32_t nw = rd32(q + hdr);
+    if ((uint64_t)hdr + 4 + 4ull * nw > avail) return -1;
+    BitRd cr{q + hdr + 4, nw, 0, 0, 0};
+    const uint32_t real = ts + 1;
+    bool gdone = false, cdone = false;   // a stream that runs out yields zeros from then on
+    uint64_t o = 0;
+    for (uint32_t t = 0; t < N; t++) {
+        uint32_t g = 0;
+        if (G > 1 && !gdone) {   // huffman_decode_idxGroup (3009-3054): root = simple node G-2
+            uint32_t node = G - 2;
+            for (;;) {
+                const int bit = gr.next();
+                if (bit < 0) { gdone = true; g = 0; break; }
+                uint32_t nx = bit ? grc[node] : glc[node];
+                if (nx < G) { g = nx; break; }
+                nx -= G;
+                if (nx + 1 >= G) return -1;
+                node = nx;
+            }
+        }
+        uint32_t ch = 0;
+        if (ts > 0 && !cdone) {
+            uint32_t node = ts - 1;
+            for (;;) {
+                const int bit = cr.next();
+                if (bit < 0) { cdone = true; ch = 0; break; }
+                const uint32_t k = 2 * node + (uint32_t)bit;
+                const uint32_t v = pairs[k];
+                if (!((bm[k >> 3] >> (k & 7)) & 1)) { ch = v; break; }
+                const uint32_t nx = v - (256 - real);
+                if (v < 256 - real || nx >= ts) return -1;
+                node = nx;
+            }
+        }
+        const uint32_t r = (G > 1 ? g * 256u : 0u) + gpos[t];   // 3586-3595
+        if (r >= wcnt) return -1;
+        const uint32_t ix = pindex[r];
+        uint32_t L = 0;
+        if (ix != 0) {   // my_LZ78_decompress (1901-1934): phrase[ix - 1] + c
+            if (ix > t) return -1;
+            L = plen[ix - 1];
+            if (o + L + 1 > cap) return -1;
+            const uint8_t *src = out + pstart[ix - 1];
+            for (uint32_t k = 0; k < L; k++) out[o + k] = src[k];
+        }
+        if (o + L + 1 > cap) return -1;
+        out[o + L] = (uint8_t)ch;
+        pstart[t] = (uint32_t)o;
+        plen[t] = L + 1;
+        o += L + 1;
+    }
+    if (o > 0 && out[o - 1] == 0) o--;   // 3701-3703
+    return (int64_t)o;
+}
+
+__global__ __launch_bounds__(64) void k78_decode(Dec78 D) {
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= D.nb) return;
+    const uint64_t B = D.B;
+    const int64_t r = dec_block(D.in + D.roff[b], D.rlen[b], D.out + b * B, B, D.pindex + b * (B + 2),
+                                D.pstart + b * B, D.plen + b * B, D.lc + (uint64_t)b * 2 * D.Gmax, D.Gmax);
+    D.dlen[b] = r < 0 ? ~0ull : (uint64_t)r;
+}
+
+__global__ __launch_bounds__(256) void k78_pack_out(Dec78 D, const uint64_t *__restrict__ doff,
+                                                    uint8_t *__restrict__ dst) {
+    const uint32_t b = blockIdx.y;
+    const uint64_t n = D.dlen[b], o = doff[b];
+    const uint8_t *src = D.out + (uint64_t)b * D.B;
+    for (uint64_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) dst[o + p] = src[p];
+}
+
+}  // namespace fcx78
+
+namespace {
+constexpr uint32_t kDecBatch = 256;
+
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+// decodes `nrec` records whose payloads sit at host `in` + roff[i] (rlen[i] bytes);
+// writes the decoded bytes densely to host `out`
+int lz78_decode_records(const uint8_t *in, uint64_t in_len, const std::vector<uint64_t> &roff,
+                        const std::vector<uint32_t> &rlen, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    const uint32_t nrec = (uint32_t)roff.size();
+    *out_len = 0;
+    if (nrec == 0) return FCX_OK;
+    const uint32_t B = FCX_MAX_BLOCK_BYTES + 8, Gmax = FCX_MAX_BLOCK_BYTES / 256 + 4;
+    const uint32_t nb = std::min(nrec, kDecBatch);
+    DevBuf din, dscr;
+    H78(hipMalloc(&din.p, in_len ? in_len : 16));
+    H78(hipMemcpy(din.p, in, in_len, hipMemcpyHostToDevice));
+    const uint64_t nbl = nb;
+    const uint64_t sz[] = {nbl * 8, nbl * 4, nbl * B, nbl * (B + 2) * 4, nbl * B * 4, nbl * B * 4,
+                           nbl * 2 * Gmax * 4, nbl * 8, nbl * 8, std::min<uint64_t>(cap, nbl * B) + 16};
+    constexpr int K = sizeof(sz) / sizeof(sz[0]);
+    uint64_t offs[K], tot = 0;
+    for (int i = 0; i < K; i++) {
+        offs[i] = tot;
+        tot += (sz[i] + 255) & ~255ull;
+    }
+    H78(hipMalloc(&dscr.p, tot));
+    char *m = (char *)dscr.p;
+    Dec78 D;
+    D.B = B;
+    D.Gmax = Gmax;
+    D.in = (const uint8_t *)din.p;
+    uint64_t *d_roff = (uint64_t *)(m + offs[0]);
+    uint32_t *d_rlen = (uint32_t *)(m + offs[1]);
+    D.roff = d_roff;
+    D.rlen = d_rlen;
+    D.out = (uint8_t *)(m + offs[2]);
+    D.pindex = (uint32_t *)(m + offs[3]);
+    D.pstart = (uint32_t *)(m + offs[4]);
+    D.plen = (uint32_t *)(m + offs[5]);
+    D.lc = (uint32_t *)(m + offs[6]);
+    D.dlen = (uint64_t *)(m + offs[7]);
+    uint64_t *d_doff = (uint64_t *)(m + offs[8]);
+    uint8_t *d_dst = (uint8_t *)(m + offs[9]);
+    std::vector<uint64_t> dl(nb), doff(nb);
+    uint64_t o = 0;
+    for (uint32_t r0 = 0; r0 < nrec; r0 += nb) {
+        D.nb = std::min(nb, nrec - r0);
+        H78(hipMemcpy(d_roff, roff.data() + r0, 8ull * D.nb, hipMemcpyHostToDevice));
+        H78(hipMemcpy(d_rlen, rlen.data() + r0, 4ull * D.nb, hipMemcpyHostToDevice));
+        k78_decode<<<(D.nb + 63) / 64, 64>>>(D);
+        H78(hipGetLastError());
+        H78(hipMemcpy(dl.data(), D.dlen, 8ull * D.nb, hipMemcpyDeviceToHost));
+        uint64_t bo = 0;
+        for (uint32_t i = 0; i < D.nb; i++) {
+            if (dl[i] == ~0ull)
+                return fail78(FCX_ERR_FORMAT, "fcx_lz78: malformed record " + std::to_string(r0 + i + 1));
+            doff[i] = bo;
+            bo += dl[i];
+        }
+        if (o + bo > cap) return fail78(FCX_ERR_CAPACITY, "fcx_lz78: decoded output exceeds capacity");
+        H78(hipMemcpy(d_doff, doff.data(), 8ull * D.nb, hipMemcpyHostToDevice));
+        k78_pack_out<<<dim3(64, D.nb), 256>>>(D, d_doff, d_dst);
+        H78(hipGetLastError());
+        H78(hipMemcpy(out + o, d_dst, bo, hipMemcpyDeviceToHost));
+        o += bo;
+    }
+    *out_len = o;
+    return FCX_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t fcx_lz78_decompress_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap) {
+    if (!in || !out) return fail78(FCX_ERR_ARG, "fcx_lz78_decompress_block: NULL argument");
+    std::vector<uint64_t> roff{0};
+    std::vector<uint32_t> rlen{len};
+    uint64_t n = 0;
+    if (int rc = lz78_decode_records(in, len, roff, rlen, out, cap, &n)) return rc;
+    return (int64_t)n;
+}
+
+int fcx_lz78_decompress_host(const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t cap, uint64_t *out_len) {
+    if (!in || !out_len || (cap && !out)) return fail78(FCX_ERR_ARG, "fcx_lz78_decompress_host: NULL argument");
+    // header check as main() (4140-4159): "FCX" magic, anything but '7' selects LZ78
+    if (in_len < FCX_HEADER_BYTES || memcmp(in, "FCX", 3) != 0 || in[3] == '7')
+        return fail78(FCX_ERR_FORMAT, "fcx_lz78_decompress_host: not an FCX8 (LZ78) stream");
+    uint16_t nblk;
+    memcpy(&nblk, in + 8, 2);
+    std::vector<uint64_t> roff;
+    std::vector<uint32_t> rlen;
+    uint64_t q = FCX_HEADER_BYTES;
+    for (uint32_t b = 0; b < nblk; b++) {
+        if (q + 4 > in_len) return fail78(FCX_ERR_FORMAT, "fcx_lz78: truncated record length");
+        uint32_t sz;
+        memcpy(&sz, in + q, 4);
+        q += 4;
+        if (q + sz > in_len) return fail78(FCX_ERR_FORMAT, "fcx_lz78: truncated record");
+        roff.push_back(q);
+        rlen.push_back(sz);
+        q += sz;
+    }
+    return lz78_decode_records(in, in_len, roff, rlen, out, cap, out_len);
 }
 
 }  // extern "C"

@@ -14,6 +14,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLI = os.path.join(ROOT, "my_compress_amd", "bin", "my_compress")
 
 
+def gpu_present() -> bool:
+    """asks the product library (its own HIP runtime), not torch: torch bundles another
+    HIP runtime, which may report no device once libfcx has initialised in-process"""
+    import ctypes
+
+    import my_compress_amd as mc
+
+    h = ctypes.c_void_p()
+    if mc.lib().fcx_dctx_create(ctypes.byref(h), 0) != 0:
+        return False
+    mc.lib().fcx_dctx_destroy(h)
+    return True
+
+
 def run(args, cwd):
     return subprocess.run([CLI] + args, cwd=cwd, capture_output=True, text=True, timeout=600)
 
@@ -31,18 +45,36 @@ def test_cli_decompresses_reference_streams(tmp_path, golden):
         assert (tmp_path / "plain").read_bytes() == data
 
 
-def test_cli_rejects_foreign_stream_and_lz78(tmp_path):
+def test_cli_rejects_foreign_stream(tmp_path):
     (tmp_path / "junk").write_bytes(b"NOTFCX" * 10)
     assert run(["-i", "junk", "-o", "x"], tmp_path).returncode != 0
-    (tmp_path / "plain").write_bytes(b"hello")
+
+
+def test_cli_lz78_fails_loudly_without_gpu(tmp_path):
+    if gpu_present():
+        pytest.skip("GPU present")
+    (tmp_path / "plain").write_bytes(b"hello hello")
     r = run(["-i", "plain", "-o", "x", "-c", "lz78"], tmp_path)
-    assert r.returncode != 0 and "scope" in r.stderr
+    assert r.returncode != 0 and ("HIP" in r.stderr or "GPU" in r.stderr)
+    (tmp_path / "x8").write_bytes(oracle.lz78_compress_file(b"hello hello", 1 << 20))
+    r = run(["-i", "x8", "-o", "y"], tmp_path)
+    assert r.returncode != 0
+
+
+@pytest.mark.gpu
+def test_cli_lz78_matches_oracle_and_round_trips(tmp_path):
+    data = inputs.mosaic(41, (2 << 20) + 4321)
+    (tmp_path / "plain").write_bytes(data)
+    r = run(["-i", "plain", "-o", "c8", "-c", "lz78"], tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert (tmp_path / "c8").read_bytes() == oracle.lz78_compress_file(data, 1 << 20)
+    r = run(["-i", "c8", "-o", "back"], tmp_path)
+    assert r.returncode == 0 and "SUCCESS" in r.stdout, r.stdout + r.stderr
+    assert (tmp_path / "back").read_bytes() == oracle.lz78_decompress_file((tmp_path / "c8").read_bytes(), len(data) + 64)
 
 
 def test_cli_compress_fails_loudly_without_gpu(tmp_path):
-    import torch
-
-    if torch.cuda.is_available():
+    if gpu_present():
         pytest.skip("GPU present")
     (tmp_path / "plain").write_bytes(b"hello hello hello hello")
     r = run(["-i", "plain", "-o", "x", "-c", "lz77"], tmp_path)

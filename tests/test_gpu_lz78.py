@@ -63,3 +63,43 @@ def test_capacity_error():
     n = ctypes.c_uint64()
     rc = mc.lib().fcx_lz78_compress_host(data, len(data), 1 << 20, out, 1000, ctypes.byref(n))
     assert rc == -2
+
+
+# ---- decoder (my_decompress_file_lz78 3478-3710) ----
+def test_decode_golden_files():
+    with open(os.path.join(HERE, "golden", "golden_lz78.json")) as f:
+        g = json.load(f)
+    for rec in g["cases"]:
+        data = inputs.make(rec)
+        dec = mc.decompress_lz78(oracle.lz78_compress_file(data, rec["block"]))
+        assert len(dec) == rec["dec_bytes"] and sha(dec) == rec["dec_sha256"], rec["name"]
+        assert (dec == data) == rec["round_trip"], rec["name"]
+
+
+@pytest.mark.parametrize("kind", ["rand", "text", "zeros", "runs"])
+def test_decode_round_trip(kind):
+    n, block = (3 << 20) + 777, 1 << 20
+    data = inputs.generate(kind, 9, n)
+    blob = mc.compress_lz78(data, block)
+    assert mc.decompress_lz78(blob) == oracle.lz78_decompress_file(blob, n + 64)
+
+
+def test_decode_small_blocks_vs_oracle():
+    data = inputs.mosaic(78, (20 << 20) + 5)
+    blob = mc.compress_lz78(data, 1 << 16)
+    assert mc.decompress_lz78(blob) == oracle.lz78_decompress_file(blob, len(data) + 64)
+
+
+def test_decode_quirks_and_malformed():
+    # tail zero dropped (3701-3703), one-symbol char stream decodes as zeros
+    assert mc.decompress_lz78(mc.compress_lz78(b"a")) == b""
+    assert mc.decompress_lz78(mc.compress_lz78(b"aaaa")) == b"aaaa"
+    assert mc.decompress_lz78(mc.compress_lz78(b"\0\0\0")) == b"\0\0"
+    p = mc.my_compress_file_lz78(inputs.mosaic(5, 5000))
+    assert mc.my_decompress_file_lz78(p) == oracle.lz78_decompress_block(p, 1 << 20)
+    with pytest.raises(mc.FcxError):
+        mc.my_decompress_file_lz78(b"\0\0\0\0")        # wcnt == 0
+    with pytest.raises(mc.FcxError):
+        mc.my_decompress_file_lz78(p[:len(p) // 2])    # truncated
+    with pytest.raises(mc.FcxError):
+        mc.decompress_lz78(mc.compress(b"abc"))         # an FCX7 stream
