@@ -7,7 +7,8 @@
 // phrase), so it runs one lane per block over an open-addressed trie in HBM.
 // Everything after the parse is position-parallel:
 //
-//   k78_parse     lane per block: trie walk -> tokens (idx[t], c[t]), N, max idx
+//   k78_parse     wave per block (lane 0 walks): trie walk -> tokens (idx[t], c[t]),
+//                 N, max idx; root children in LDS, depth-1 children dense, deeper hashed
 //   k78_mark      token-parallel: bitmap of used indices (3180-3206), char histogram
 //   k78_rank      workgroup per block: popcount prefix of the bitmap -> rank base per
 //                 word, wcnt (mapIdx 3216-3219)
@@ -49,6 +50,7 @@ struct Rec78 {
 struct Scratch {
     uint32_t B, nb, cap_log2, Gmax, tiles;
     uint64_t *slot;      // nb << cap_log2
+    uint32_t *d1;        // nb << 16 (depth-1 children, dense)
     uint32_t *idx;       // nb * B
     uint8_t *c;          // nb * B
     uint32_t *bm;        // nb * bmw
@@ -80,9 +82,16 @@ __device__ inline uint64_t trie_hash(uint64_t key) { return (key * 0x9E3779B97F4
 // my_LZ78_compress (1832-1899): phrase = longest dictionary prefix + 1 byte; token
 // (prefix index or 0, byte); the phrase enters the dictionary at the next index.  A
 // block whose remainder is a dictionary string ends with (its index, 0) (1858-1863).
+// The dictionary is a set of strings with ids, so it can be held as three tables
+// with the same contents as one trie: the root's children in LDS (256 ids), the
+// depth-1 children as a dense 256x256 table per block (256 KiB, L2/MALL-resident),
+// deeper children in the open-addressed hash table.  One wave per block, lane 0 walks.
 __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, uint64_t n, Scratch S, uint64_t base_blk) {
-    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= S.nb) return;
+    __shared__ uint32_t root[256];
+    const uint32_t b = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < 256; i += 64) root[i] = 0;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     const uint64_t off = (base_blk + b) * (uint64_t)S.B;
     Rec78 &R = S.rec[b];
     if (off >= n) {
@@ -92,30 +101,40 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
     const uint32_t len = (uint32_t)min((uint64_t)S.B, n - off);
     const uint8_t *src = in + off;
     uint64_t *slot = S.slot + ((uint64_t)b << S.cap_log2);
+    uint32_t *d1 = S.d1 + ((uint64_t)b << 16);
     const uint64_t mask = (1ull << S.cap_log2) - 1;
     uint32_t *idx = S.idx + (uint64_t)b * S.B;
     uint8_t *cc = S.c + (uint64_t)b * S.B;
     uint32_t N = 0, next = 1, pos = 0, maxi = 0;
     while (pos < len) {
-        uint32_t node = 0;
+        uint32_t node = 0, depth = 0, first = 0;
         bool put = false;
         uint64_t h = 0, key = 0;
         while (pos < len) {
-            key = (((uint64_t)node << 8) | src[pos]) + 1;
+            const uint32_t byte = src[pos];
             uint32_t child = 0;
-            for (h = trie_hash(key) & mask;; h = (h + 1) & mask) {
-                const uint64_t s = slot[h];
-                if (s == 0) break;
-                if ((s >> 24) == key) {
-                    child = (uint32_t)(s & 0xFFFFFFu);
-                    break;
+            if (depth == 0) {
+                child = root[byte];
+                first = byte;
+            } else if (depth == 1) {
+                child = d1[(first << 8) | byte];
+            } else {
+                key = (((uint64_t)node << 8) | byte) + 1;
+                for (h = trie_hash(key) & mask;; h = (h + 1) & mask) {
+                    const uint64_t s = slot[h];
+                    if (s == 0) break;
+                    if ((s >> 24) == key) {
+                        child = (uint32_t)(s & 0xFFFFFFu);
+                        break;
+                    }
                 }
             }
             if (!child) {
-                put = true;   // h is the empty slot that ended the probe
+                put = true;   // for depth >= 2, h is the empty slot that ended the probe
                 break;
             }
             node = child;
+            depth++;
             pos++;
         }
         if (!put) {   // whole remainder found
@@ -125,9 +144,13 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
             maxi = max(maxi, node);
             break;
         }
-        slot[h] = (key << 24) | next++;
+        const uint32_t byte = src[pos];
+        if (depth == 0) root[byte] = next;
+        else if (depth == 1) d1[(first << 8) | byte] = next;
+        else slot[h] = (key << 24) | next;
+        next++;
         idx[N] = node;
-        cc[N] = src[pos];
+        cc[N] = (uint8_t)byte;
         N++;
         maxi = max(maxi, node);
         pos++;
@@ -590,7 +613,7 @@ int setup(Alloc78 &A, uint32_t B, uint32_t nb) {
         (nbl << S.cap_log2) * 8, nbl * B * 4, nbl * B, nbl * S.bmw * 4, nbl * S.bmw * 4, nbl * B * 2, nbl * B,
         nbl * S.Gmax * 4, nbl * 256 * 4, nbl * S.Gmax * 4, nbl * S.Gmax, nbl * 256 * 4, nbl * 256,
         nbl * 2 * S.Gmax * 4, nbl * 2 * S.Gmax * 4, nbl * S.Gmax * 4, nbl * 576, nbl * S.tiles * 8,
-        nbl * (B + 2) * 4, nbl * (B + 2) * 4, nbl * sizeof(Rec78), nbl * 8, 8};
+        nbl * (B + 2) * 4, nbl * (B + 2) * 4, nbl * sizeof(Rec78), nbl * 8, 8, (nbl << 16) * 4};
     constexpr int K = sizeof(sz) / sizeof(sz[0]);
     uint64_t offs[K], tot = 0;
     for (int i = 0; i < K; i++) {
@@ -622,6 +645,7 @@ int setup(Alloc78 &A, uint32_t B, uint32_t nb) {
     S.rec = (Rec78 *)(m + offs[20]);
     S.off = (uint64_t *)(m + offs[21]);
     S.total = (uint64_t *)(m + offs[22]);
+    S.d1 = (uint32_t *)(m + offs[23]);
     return FCX_OK;
 }
 
@@ -656,13 +680,14 @@ int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_byte
         S.nb = (uint32_t)std::min<uint64_t>(batch, nblk - b0);
         const uint32_t nb = S.nb;
         H78(hipMemsetAsync(S.slot, 0, ((uint64_t)nb << S.cap_log2) * 8, st));
+        H78(hipMemsetAsync(S.d1, 0, ((uint64_t)nb << 16) * 4, st));
         H78(hipMemsetAsync(S.bm, 0, (uint64_t)nb * S.bmw * 4, st));
         H78(hipMemsetAsync(S.gcnt, 0, (uint64_t)nb * S.Gmax * 4, st));
         H78(hipMemsetAsync(S.chist, 0, (uint64_t)nb * 256 * 4, st));
         H78(hipMemsetAsync(S.gstage, 0, (uint64_t)nb * (S.B + 2) * 4, st));
         H78(hipMemsetAsync(S.cstage, 0, (uint64_t)nb * (S.B + 2) * 4, st));
         const dim3 tok_grid(S.tiles, nb);
-        k78_parse<<<(nb + 63) / 64, 64, 0, st>>>(d_in, n, S, b0);
+        k78_parse<<<nb, 64, 0, st>>>(d_in, n, S, b0);
         k78_mark<<<tok_grid, 256, 0, st>>>(S);
         k78_rank<<<nb, 1024, 0, st>>>(S);
         k78_group<<<tok_grid, 256, 0, st>>>(S);
@@ -886,9 +911,9 @@ __device__ int64_t dec_block(const uint8_t *in, uint32_t len, uint8_t *out, uint
     return (int64_t)o;
 }
 
-__global__ __launch_bounds__(64) void k78_decode(Dec78 D) {
-    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= D.nb) return;
+__global__ __launch_bounds__(64) void k78_decode(Dec78 D) {   // one wave per record, lane 0 decodes
+    const uint32_t b = blockIdx.x;
+    if (b >= D.nb || threadIdx.x != 0) return;
     const uint64_t B = D.B;
     const int64_t r = dec_block(D.in + D.roff[b], D.rlen[b], D.out + b * B, B, D.pindex + b * (B + 2),
                                 D.pstart + b * B, D.plen + b * B, D.lc + (uint64_t)b * 2 * D.Gmax, D.Gmax);
@@ -960,7 +985,7 @@ int lz78_decode_records(const uint8_t *in, uint64_t in_len, const std::vector<ui
         D.nb = std::min(nb, nrec - r0);
         H78(hipMemcpy(d_roff, roff.data() + r0, 8ull * D.nb, hipMemcpyHostToDevice));
         H78(hipMemcpy(d_rlen, rlen.data() + r0, 4ull * D.nb, hipMemcpyHostToDevice));
-        k78_decode<<<(D.nb + 63) / 64, 64>>>(D);
+        k78_decode<<<D.nb, 64>>>(D);
         H78(hipGetLastError());
         H78(hipMemcpy(dl.data(), D.dlen, 8ull * D.nb, hipMemcpyDeviceToHost));
         uint64_t bo = 0;
