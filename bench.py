@@ -312,6 +312,60 @@ def cpu_baseline(kind, seed, block, threads=16, nblocks=32, nblocks_1t=4):
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count()}
 
 
+def lz78_leg(dev, mib=256, block=1 << 20, reps=2, ref_blocks=2):
+    """the -c lz78 codec (fcx_lz78.hip; my_compress_file_lz78 :3127) on a device-resident
+    rand shard: compress rate, the first `ref_blocks` records checked against the
+    reference compiled in place (the oracle when it is absent), and the reference timed
+    on the same blocks on one core (it is single-threaded)"""
+    import torch
+
+    import inputs
+    import my_compress_amd as mc
+    import oracle
+
+    n = mib << 20
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    inputs.generate_into("rand", 4, host.data_ptr(), n)
+    d_in = host.to(dev)
+    cap = mc.lz78_bound(n, block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    out_len = ctypes.c_uint64()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    L = mc.lib()
+    times = []
+    for it in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        rc = L.fcx_lz78_compress_shard(d_in.data_ptr(), n, block, d_out.data_ptr(), cap, ctypes.byref(out_len), st)
+        torch.cuda.synchronize(dev)
+        if rc != 0:
+            raise RuntimeError(L.fcx_last_error().decode())
+        if it:
+            times.append(time.perf_counter() - t0)
+    dt = sum(times) / len(times)
+    head = d_out[:min(out_len.value, ref_blocks * (2 * block + 65536))].cpu().numpy().tobytes()
+    R = oracle.ref()
+    blocks = [bytes(host[i * block:(i + 1) * block].numpy()) for i in range(ref_blocks)]
+    if R is not None:
+        R.ref_set_quiet(1)
+    t1 = time.perf_counter()
+    want = [oracle.ref_lz78_compress_block(b) if R is not None else oracle.lz78_compress_block(b) for b in blocks]
+    cpu_s = time.perf_counter() - t1
+    if R is not None:
+        R.ref_set_quiet(0)
+    q, exact = 0, True
+    for w in want:
+        sz = int.from_bytes(head[q:q + 4], "little")
+        exact &= head[q + 4:q + 4 + sz] == w
+        q += 4 + sz
+    return {"value": n / dt / 1e6, "unit": "MB/s", "ms_per_step": dt * 1e3, "ratio": out_len.value / n,
+            "workload": f"rand {mib} MiB, {block // 1024} KiB blocks, device-resident",
+            "bit_exact_first_blocks": exact, "checked_blocks": ref_blocks,
+            "cpu_baseline": {"value": ref_blocks * block / cpu_s / 1e6, "unit": "MB/s", "cores": 1,
+                             "kind": "reference" if R is not None else "port",
+                             "sample": f"first {ref_blocks} x {block // 1024} KiB blocks, my_compress_file_lz78"}}
+
+
 def load_pmc(path):
     if path and os.path.exists(path):
         with open(path) as f:
@@ -337,6 +391,7 @@ def main():
     ap.add_argument("--no-host-path", dest="host_path", action="store_false",
                     help="skip the host-to-host (PCIe-inclusive) timing of the main leg")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-lz78", action="store_true", help="skip the -c lz78 codec leg")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     args = ap.parse_args()
 
@@ -407,6 +462,8 @@ def main():
             "decode": main_res.get("decode"),
             "host_path": main_res.get("host_path"),
         }
+        if world == 1 and not args.no_lz78 and not args.no_text:
+            line["lz78"] = lz78_leg(dev)
         for name, lr in legs.items():
             line[name] = {k: lr[k] for k in ["value", "ms_per_step", "ratio", "block_bytes", "stages_ms", "lazy_evals"]}
             if "decode" in lr:
