@@ -312,7 +312,7 @@ def cpu_baseline(kind, seed, block, threads=16, nblocks=32, nblocks_1t=4):
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count()}
 
 
-def lz78_leg(dev, mib=256, block=1 << 20, reps=2, ref_blocks=2):
+def lz78_leg(dev, mib=1024, block=1 << 20, reps=2, ref_blocks=2):
     """the -c lz78 codec (fcx_lz78.hip; my_compress_file_lz78 :3127) on a device-resident
     rand shard: compress rate, the first `ref_blocks` records checked against the
     reference compiled in place (the oracle when it is absent), and the reference timed

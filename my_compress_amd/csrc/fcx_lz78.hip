@@ -649,8 +649,10 @@ int setup(Alloc78 &A, uint32_t B, uint32_t nb) {
     return FCX_OK;
 }
 
-// scratch footprint per block is ~50 B per input byte (trie 32 B): batches keep it bounded
-constexpr uint64_t kBatchBytes = 256ull << 20;
+// scratch is ~50 B per input byte of a batch (the trie 32 B): 1 GiB batches (~50 GB of
+// HBM) because the parse has one walker per block and rate grows with walkers in flight
+// (256 MiB: 539 MB/s, 1 GiB: 1386 MB/s on rand)
+constexpr uint64_t kBatchBytes = 1024ull << 20;
 }  // namespace
 
 extern "C" {
