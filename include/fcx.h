@@ -167,13 +167,16 @@ int fcx_dctx_stage(fcx_dctx *ctx, int i, const char **name, float *ms);
  *   fcx_lz78_compress_host   <- the whole -c lz78 compress mode of main()            :4073-4136
  * Same record framing as FCX7 ([u32 len][payload] per block); the payload layout is
  * my_compress_file_lz78's.  GPU-only like the LZ77 path (FCX_ERR_HIP without a device).
- * Scratch is allocated per call (~50 B per input byte of a batch of <= 1 GiB). */
+ * Compress scratch (~50 B per input byte of a batch of <= 1 GiB) is kept per device
+ * between calls; calls on one device are serialised; fcx_lz78_release() frees it. */
 /* d_in / d_out device pointers; writes the records (no header) and their length. */
 int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_bytes, uint8_t *d_out, uint64_t cap,
                             uint64_t *out_len, void *stream);
 /* host buffers; writes the "FCX8" header (total mod 2^32, u16 block count) + records. */
 int fcx_lz78_compress_host(const uint8_t *in, uint64_t n, uint32_t block_bytes, uint8_t *out, uint64_t cap,
                            uint64_t *out_len);
+/* frees the current device's LZ78 compress scratch */
+int fcx_lz78_release(void);
 /* one block: payload bytes (no length prefix), 0 on NULL / error; out >= 10*len + 4096. */
 uint32_t fcx_lz78_compress_block(const void *in, uint32_t len, uint8_t *out);
 /*   fcx_lz78_decompress_block <- my_decompress_file_lz78(void*, uInt32, FILE*)       :3478 (called at :4189)

@@ -28,6 +28,7 @@
 
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <vector>
 #include <algorithm>
 
@@ -593,12 +594,25 @@ int fail78(int code, const std::string &m) {
 struct Alloc78 {
     Scratch S{};
     void *mem = nullptr;
-    ~Alloc78() {
-        if (mem) (void)hipFree(mem);
-    }
 };
 
-int setup(Alloc78 &A, uint32_t B, uint32_t nb) {
+// Compress scratch is kept per device between calls (grow-only; ~50 GB for a 1 GiB
+// batch), so repeated shards do not pay hipMalloc/hipFree; fcx_lz78_release frees it.
+// Calls on one device are serialised on its slot.
+struct Cache78 {
+    std::mutex mu;
+    void *mem = nullptr;
+    uint64_t bytes = 0;
+};
+Cache78 g_cache[64];
+
+Cache78 *cache_for_current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    return &g_cache[dev];
+}
+
+int setup(Alloc78 &A, Cache78 &C, uint32_t B, uint32_t nb) {
     Scratch &S = A.S;
     S.B = B;
     S.nb = nb;
@@ -620,7 +634,14 @@ int setup(Alloc78 &A, uint32_t B, uint32_t nb) {
         offs[i] = tot;
         tot += (sz[i] + 255) & ~255ull;
     }
-    H78(hipMalloc(&A.mem, tot));
+    if (C.bytes < tot) {
+        if (C.mem) (void)hipFree(C.mem);
+        C.mem = nullptr;
+        C.bytes = 0;
+        H78(hipMalloc(&C.mem, tot));
+        C.bytes = tot;
+    }
+    A.mem = C.mem;
     char *m = (char *)A.mem;
     S.slot = (uint64_t *)(m + offs[0]);
     S.idx = (uint32_t *)(m + offs[1]);
@@ -667,8 +688,11 @@ int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_byte
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nblk = (n + block_bytes - 1) / block_bytes;
     const uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nblk, kBatchBytes / block_bytes));
+    Cache78 *C = cache_for_current_device();
+    if (!C) return fail78(FCX_ERR_HIP, "fcx_lz78_compress_shard: no current HIP device");
+    std::lock_guard<std::mutex> lock(C->mu);
     Alloc78 A;
-    if (int rc = setup(A, block_bytes, batch)) return rc;
+    if (int rc = setup(A, *C, block_bytes, batch)) return rc;
     Scratch S = A.S;
     uint32_t *d_err = nullptr;
     H78(hipMalloc(&d_err, 4));
@@ -709,6 +733,16 @@ int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_byte
     if (herr & 2) return fail78(FCX_ERR_CAPACITY, "fcx_lz78_compress_shard: output capacity exceeded");
     if (herr & 1) return fail78(FCX_ERR_INTERNAL, "fcx_lz78_compress_shard: Huffman code longer than 32 bits");
     *out_len = total;
+    return FCX_OK;
+}
+
+int fcx_lz78_release(void) {
+    Cache78 *C = cache_for_current_device();
+    if (!C) return fail78(FCX_ERR_HIP, "fcx_lz78_release: no current HIP device");
+    std::lock_guard<std::mutex> lock(C->mu);
+    if (C->mem) H78(hipFree(C->mem));
+    C->mem = nullptr;
+    C->bytes = 0;
     return FCX_OK;
 }
 
@@ -933,7 +967,7 @@ __global__ __launch_bounds__(256) void k78_pack_out(Dec78 D, const uint64_t *__r
 }  // namespace fcx78
 
 namespace {
-constexpr uint32_t kDecBatch = 256;
+constexpr uint32_t kDecBatch = 1024;   // records decoded concurrently (one walker each; ~13 MB of scratch per record)
 
 struct DevBuf {
     void *p = nullptr;
