@@ -343,6 +343,7 @@ def lz78_leg(dev, mib=1024, block=1 << 20, reps=2, ref_blocks=2):
         if it:
             times.append(time.perf_counter() - t0)
     dt = sum(times) / len(times)
+    mc.lz78_release()
     head = d_out[:min(out_len.value, ref_blocks * (2 * block + 65536))].cpu().numpy().tobytes()
     R = oracle.ref()
     blocks = [bytes(host[i * block:(i + 1) * block].numpy()) for i in range(ref_blocks)]

@@ -95,6 +95,7 @@ def lib():
                                          ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_lz78_compress_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, c_u8p]
     L.fcx_lz78_compress_block.restype = ctypes.c_uint32
+    L.fcx_lz78_release.argtypes = []
     L.fcx_lz78_decompress_block.argtypes = [c_u8p, ctypes.c_uint32, c_u8p, ctypes.c_uint64]
     L.fcx_lz78_decompress_block.restype = ctypes.c_int64
     L.fcx_lz78_decompress_host.argtypes = [c_u8p, ctypes.c_uint64, c_u8p, ctypes.c_uint64,
@@ -377,3 +378,8 @@ def decompress_lz78(blob: bytes, cap: int = None) -> bytes:
     n = ctypes.c_uint64()
     _check(lib().fcx_lz78_decompress_host(blob, len(blob), out, cap, ctypes.byref(n)), "fcx_lz78_decompress_host")
     return out.raw[:n.value]
+
+
+def lz78_release() -> None:
+    """frees the LZ78 compress scratch cached on the current HIP device"""
+    _check(lib().fcx_lz78_release(), "fcx_lz78_release")
