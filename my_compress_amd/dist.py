@@ -1,4 +1,5 @@
-"""Multi-GPU sharding of the FCX7 compress path.
+"""Multi-GPU sharding of the FCX7 compress path (and of FCX8, the -c lz78 codec,
+whose records are framed the same way).
 
 Blocks are independent (the window and the parse restart per block,
 my_compress.cpp:1675-1703, and main() zeroes its buffers between blocks,
@@ -42,6 +43,11 @@ def concat_segments(seg: torch.Tensor, dist, group=None) -> torch.Tensor:
     return torch.cat([recv[r][:szs[r]] for r in range(world)])
 
 
-def assemble_file(total_in: int, block_bytes: int, body: bytes) -> bytes:
+def assemble_file(total_in: int, block_bytes: int, body: bytes, codec: str = "lz77") -> bytes:
+    """header + concatenated records; codec "lz78" writes the "FCX8" tag (-c lz78 files,
+    same framing, main() 4079-4086)"""
     nblocks = (total_in + block_bytes - 1) // block_bytes
-    return write_header(total_in, nblocks) + body
+    hdr = write_header(total_in, nblocks)
+    if codec == "lz78":
+        hdr = b"FCX8" + hdr[4:]
+    return hdr + body

@@ -32,11 +32,12 @@ def _worker(rank, world, port, cases, results):
         for idx, (spec, block) in enumerate(cases):
             data = inputs.make(spec)
             lo, hi = fdist.byte_range(len(data), block, rank, world)
-            seg = oracle.compress_file(data[lo:hi], block)[10:] if hi > lo else b""
-            t = torch.frombuffer(bytearray(seg), dtype=torch.uint8) if seg else torch.zeros(0, dtype=torch.uint8)
-            whole = fdist.concat_segments(t, dist)
-            if rank == 0:
-                results[idx] = fdist.assemble_file(len(data), block, whole.numpy().tobytes())
+            for codec, enc in (("lz77", oracle.compress_file), ("lz78", oracle.lz78_compress_file)):
+                seg = enc(data[lo:hi], block)[10:] if hi > lo else b""
+                t = torch.frombuffer(bytearray(seg), dtype=torch.uint8) if seg else torch.zeros(0, dtype=torch.uint8)
+                whole = fdist.concat_segments(t, dist)
+                if rank == 0:
+                    results[(idx, codec)] = fdist.assemble_file(len(data), block, whole.numpy().tobytes(), codec)
     finally:
         dist.destroy_process_group()
 
@@ -53,7 +54,8 @@ def test_two_rank_concat_matches_single_process():
     mp.spawn(_worker, args=(2, _free_port(), cases, results), nprocs=2, join=True)
     for idx, (spec, block) in enumerate(cases):
         data = inputs.make(spec)
-        assert results[idx] == oracle.compress_file(data, block), idx
+        assert results[(idx, "lz77")] == oracle.compress_file(data, block), idx
+        assert results[(idx, "lz78")] == oracle.lz78_compress_file(data, block), idx
 
 
 def test_block_ranges_partition():
