@@ -107,53 +107,62 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
     uint32_t *idx = S.idx + (uint64_t)b * S.B;
     uint8_t *cc = S.c + (uint64_t)b * S.B;
     uint32_t N = 0, next = 1, pos = 0, maxi = 0;
+    auto emit = [&](uint32_t node, uint32_t ch) {
+        idx[N] = node;
+        cc[N] = (uint8_t)ch;
+        N++;
+        maxi = max(maxi, node);
+    };
     while (pos < len) {
-        uint32_t node = 0, depth = 0, first = 0;
+        // a phrase's first two bytes are known when it starts: their loads and the
+        // depth-1 lookup issue together, so the dependent chain per phrase is one input
+        // load, one depth-1 load, then the hashed levels
+        const uint32_t b0 = src[pos], b1 = pos + 1 < len ? src[pos + 1] : 0u;
+        const uint32_t c0 = root[b0], c1 = d1[(b0 << 8) | b1];
+        if (!c0) {   // new 1-byte phrase
+            root[b0] = next++;
+            emit(0, b0);
+            pos += 1;
+            continue;
+        }
+        if (pos + 1 == len) {   // whole remainder is a dictionary string (1858-1863)
+            emit(c0, 0);
+            break;
+        }
+        if (!c1) {   // new 2-byte phrase
+            d1[(b0 << 8) | b1] = next++;
+            emit(c0, b1);
+            pos += 2;
+            continue;
+        }
+        uint32_t node = c1;
+        pos += 2;
         bool put = false;
         uint64_t h = 0, key = 0;
         while (pos < len) {
-            const uint32_t byte = src[pos];
+            key = (((uint64_t)node << 8) | src[pos]) + 1;
             uint32_t child = 0;
-            if (depth == 0) {
-                child = root[byte];
-                first = byte;
-            } else if (depth == 1) {
-                child = d1[(first << 8) | byte];
-            } else {
-                key = (((uint64_t)node << 8) | byte) + 1;
-                for (h = trie_hash(key) & mask;; h = (h + 1) & mask) {
-                    const uint64_t s = slot[h];
-                    if (s == 0) break;
-                    if ((s >> 24) == key) {
-                        child = (uint32_t)(s & 0xFFFFFFu);
-                        break;
-                    }
+            for (h = trie_hash(key) & mask;; h = (h + 1) & mask) {
+                const uint64_t s = slot[h];
+                if (s == 0) break;
+                if ((s >> 24) == key) {
+                    child = (uint32_t)(s & 0xFFFFFFu);
+                    break;
                 }
             }
             if (!child) {
-                put = true;   // for depth >= 2, h is the empty slot that ended the probe
+                put = true;   // h is the empty slot that ended the probe
                 break;
             }
             node = child;
-            depth++;
             pos++;
         }
         if (!put) {   // whole remainder found
-            idx[N] = node;
-            cc[N] = 0;
-            N++;
-            maxi = max(maxi, node);
+            emit(node, 0);
             break;
         }
-        const uint32_t byte = src[pos];
-        if (depth == 0) root[byte] = next;
-        else if (depth == 1) d1[(first << 8) | byte] = next;
-        else slot[h] = (key << 24) | next;
-        next++;
-        idx[N] = node;
-        cc[N] = (uint8_t)byte;
-        N++;
-        maxi = max(maxi, node);
+        slot[h] = (key << 24) | next++;
+        emit(node, src[pos]);
         pos++;
     }
     R.N = N;
