@@ -118,6 +118,7 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
         // depth-1 lookup issue together, so the dependent chain per phrase is one input
         // load, one depth-1 load, then the hashed levels
         const uint32_t b0 = src[pos], b1 = pos + 1 < len ? src[pos + 1] : 0u;
+        const uint32_t b2 = pos + 2 < len ? src[pos + 2] : 0u, b3 = pos + 3 < len ? src[pos + 3] : 0u;
         const uint32_t c0 = root[b0], c1 = d1[(b0 << 8) | b1];
         if (!c0) {   // new 1-byte phrase
             root[b0] = next++;
@@ -139,8 +140,12 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
         pos += 2;
         bool put = false;
         uint64_t h = 0, key = 0;
+        uint32_t ahead = b2 | (b3 << 8), nahead = 2;   // bytes already loaded past the first two
         while (pos < len) {
-            key = (((uint64_t)node << 8) | src[pos]) + 1;
+            const uint32_t byte = nahead ? (ahead & 0xFF) : src[pos];
+            ahead >>= 8;
+            nahead -= nahead ? 1 : 0;
+            key = (((uint64_t)node << 8) | byte) + 1;
             uint32_t child = 0;
             for (h = trie_hash(key) & mask;; h = (h + 1) & mask) {
                 const uint64_t s = slot[h];
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
             break;
         }
         slot[h] = (key << 24) | next++;
-        emit(node, src[pos]);
+        emit(node, (uint32_t)((key - 1) & 0xFF));
         pos++;
     }
     R.N = N;
