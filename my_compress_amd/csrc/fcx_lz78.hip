@@ -859,7 +859,8 @@ struct BitRd {   // LSB-first u32 words, W of them
 };
 
 __device__ int64_t dec_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap, uint32_t *pindex,
-                             uint32_t *pstart, uint32_t *plen, uint32_t *glc, uint32_t Gmax) {
+                             uint32_t *pstart, uint32_t *plen, uint32_t *glc, uint32_t Gmax, uint8_t *tpairs,
+                             uint8_t *tbm) {
     const uint8_t *q = in, *end = in + len;
     if (len < 4) return -1;
     const uint32_t wcnt = rd32(q);
@@ -905,7 +906,10 @@ __device__ int64_t dec_block(const uint8_t *in, uint32_t len, uint8_t *out, uint
     if (avail < 1) return -1;
     const uint32_t ts = q[0], nbm = (2 * ts + 7) / 8, hdr = 1 + nbm + 2 * ts;
     if (avail < hdr + 4) return -1;
-    const uint8_t *bm = q + 1, *pairs = q + 1 + nbm;
+    // the char tree is walked bit by bit: copy it to LDS (tpairs / tbm) first
+    for (uint32_t k = 0; k < 2 * ts; k++) tpairs[k] = q[1 + nbm + k];
+    for (uint32_t k = 0; k < nbm; k++) tbm[k] = q[1 + k];
+    const uint8_t *bm = tbm, *pairs = tpairs;
     const uint32_t nw = rd32(q + hdr);
     if ((uint64_t)hdr + 4 + 4ull * nw > avail) return -1;
     BitRd cr{q + hdr + 4, nw, 0, 0, 0};
@@ -961,12 +965,17 @@ __device__ int64_t dec_block(const uint8_t *in, uint32_t len, uint8_t *out, uint
     return (int64_t)o;
 }
 
+constexpr uint32_t kDecGmax = FCX_MAX_BLOCK_BYTES / 256 + 4;   // groups of a <= 1 MiB block
+
 __global__ __launch_bounds__(64) void k78_decode(Dec78 D) {   // one wave per record, lane 0 decodes
     const uint32_t b = blockIdx.x;
+    // group tree children (2 x Gmax) and the char tree live in LDS for the bit walks
+    __shared__ uint32_t gtree[2 * kDecGmax];
+    __shared__ uint8_t tpairs[512], tbm[64];
     if (b >= D.nb || threadIdx.x != 0) return;
     const uint64_t B = D.B;
     const int64_t r = dec_block(D.in + D.roff[b], D.rlen[b], D.out + b * B, B, D.pindex + b * (B + 2),
-                                D.pstart + b * B, D.plen + b * B, D.lc + (uint64_t)b * 2 * D.Gmax, D.Gmax);
+                                D.pstart + b * B, D.plen + b * B, gtree, kDecGmax, tpairs, tbm);
     D.dlen[b] = r < 0 ? ~0ull : (uint64_t)r;
 }
 
@@ -997,7 +1006,7 @@ int lz78_decode_records(const uint8_t *in, uint64_t in_len, const std::vector<ui
     const uint32_t nrec = (uint32_t)roff.size();
     *out_len = 0;
     if (nrec == 0) return FCX_OK;
-    const uint32_t B = FCX_MAX_BLOCK_BYTES + 8, Gmax = FCX_MAX_BLOCK_BYTES / 256 + 4;
+    const uint32_t B = FCX_MAX_BLOCK_BYTES + 8, Gmax = 1;   // group trees live in LDS (k78_decode)
     const uint32_t nb = std::min(nrec, kDecBatch);
     DevBuf din, dscr;
     H78(hipMalloc(&din.p, in_len ? in_len : 16));
