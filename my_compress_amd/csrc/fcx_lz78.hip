@@ -867,10 +867,10 @@ __device__ int64_t dec_block(const uint8_t *in, uint32_t len, uint8_t *out, uint
     q += 4;
     if (wcnt == 0 || wcnt > cap + 2) return -1;   // the reference reads pIndex[-1] (3502)
     {   // 3494-3500: indices of the set bits, ascending
-        uint32_t i = 0;
-        for (uint64_t v = 0; i < wcnt; v++) {
-            if ((uint64_t)(end - q) <= (v >> 3)) return -1;
-            if ((q[v >> 3] >> (v & 7)) & 1) pindex[i++] = (uint32_t)v;
+        uint32_t i = 0;   // byte at a time, set bits by find-first-set
+        for (uint64_t v8 = 0; i < wcnt; v8++) {
+            if ((uint64_t)(end - q) <= v8) return -1;
+            for (uint32_t x = q[v8]; x && i < wcnt; x &= x - 1) pindex[i++] = (uint32_t)(8 * v8 + __ffs(x) - 1);
         }
     }
     q += pindex[wcnt - 1] / 8 + 1;
