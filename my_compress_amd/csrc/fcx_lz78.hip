@@ -688,6 +688,7 @@ int setup(Alloc78 &A, Cache78 &C, uint32_t B, uint32_t nb) {
 // HBM) because the parse has one walker per block and rate grows with walkers in flight
 // (256 MiB: 539 MB/s, 1 GiB: 1386 MB/s on rand)
 constexpr uint64_t kBatchBytes = 1024ull << 20;
+constexpr uint64_t kScratchBudget = 64ull << 30;
 }  // namespace
 
 extern "C" {
@@ -701,7 +702,15 @@ int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_byte
     if (n == 0) return FCX_OK;
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nblk = (n + block_bytes - 1) / block_bytes;
-    const uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nblk, kBatchBytes / block_bytes));
+    // blocks per batch: <= 1 GiB of input, and per-block scratch (trie, dense depth-1
+    // table, group tables: large for tiny blocks) within a 64 GiB budget
+    uint32_t cl2 = 10;
+    while ((1ull << cl2) < 2ull * block_bytes + 2) cl2++;
+    const uint64_t per_block = (8ull << cl2) + (1ull << 18) + 64ull * std::max<uint32_t>(1024, block_bytes / 256 + 2) +
+                               24ull * block_bytes + 4096;
+    const uint64_t by_budget = std::max<uint64_t>(1, kScratchBudget / per_block);
+    const uint32_t batch = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(std::min<uint64_t>(nblk, kBatchBytes / block_bytes), by_budget));
     Cache78 *C = cache_for_current_device();
     if (!C) return fail78(FCX_ERR_HIP, "fcx_lz78_compress_shard: no current HIP device");
     std::lock_guard<std::mutex> lock(C->mu);

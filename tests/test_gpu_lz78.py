@@ -103,3 +103,13 @@ def test_decode_quirks_and_malformed():
         mc.my_decompress_file_lz78(p[:len(p) // 2])    # truncated
     with pytest.raises(mc.FcxError):
         mc.decompress_lz78(mc.compress(b"abc"))         # an FCX7 stream
+
+
+@pytest.mark.parametrize("block", [1, 7, 1000, 4096])
+def test_tiny_blocks_vs_oracle(block):
+    # degenerate block sizes: thousands of records, per-block scratch bounded by the budget
+    data = inputs.mosaic(90 + block, 5000 if block < 100 else 3_000_001)
+    blob = mc.compress_lz78(data, block)
+    assert blob == oracle.lz78_compress_file(data, block)
+    assert mc.decompress_lz78(blob, len(data) + 64 * ((len(data) + block - 1) // block)) == \
+        oracle.lz78_decompress_file(blob, len(data) + 64 * ((len(data) + block - 1) // block))
