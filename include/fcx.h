@@ -167,7 +167,7 @@ int fcx_dctx_stage(fcx_dctx *ctx, int i, const char **name, float *ms);
  *   fcx_lz78_compress_host   <- the whole -c lz78 compress mode of main()            :4073-4136
  * Same record framing as FCX7 ([u32 len][payload] per block); the payload layout is
  * my_compress_file_lz78's.  GPU-only like the LZ77 path (FCX_ERR_HIP without a device).
- * Compress scratch (~50 B per input byte of a batch of <= 1 GiB) is kept per device
+ * Compress scratch (~40 B per input byte of a batch of <= 1 GiB) is kept per device
  * between calls; calls on one device are serialised; fcx_lz78_release() frees it. */
 /* d_in / d_out device pointers; writes the records (no header) and their length. */
 int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_bytes, uint8_t *d_out, uint64_t cap,

@@ -610,7 +610,7 @@ struct Alloc78 {
     void *mem = nullptr;
 };
 
-// Compress scratch is kept per device between calls (grow-only; ~50 GB for a 1 GiB
+// Compress scratch is kept per device between calls (grow-only; ~40 GB for a 1 GiB
 // batch), so repeated shards do not pay hipMalloc/hipFree; fcx_lz78_release frees it.
 // Calls on one device are serialised on its slot.
 struct Cache78 {
@@ -631,7 +631,9 @@ int setup(Alloc78 &A, Cache78 &C, uint32_t B, uint32_t nb) {
     S.B = B;
     S.nb = nb;
     S.cap_log2 = 10;
-    while ((1ull << S.cap_log2) < 2ull * B + 2) S.cap_log2++;
+    // only phrases of >= 3 bytes reach the hash table, so it holds <= B/3 entries:
+    // B + 2 slots keep the load <= 1/3 and always leave an empty slot
+    while ((1ull << S.cap_log2) < (uint64_t)B + 2) S.cap_log2++;
     S.Gmax = B / 256 + 2;
     if (S.Gmax < 1024) S.Gmax = 1024;   // the char tree borrows iw[0..511]; parents need 2*256
     S.tiles = (B + 1 + kTileTok - 1) / kTileTok;
@@ -684,7 +686,7 @@ int setup(Alloc78 &A, Cache78 &C, uint32_t B, uint32_t nb) {
     return FCX_OK;
 }
 
-// scratch is ~50 B per input byte of a batch (the trie 32 B): 1 GiB batches (~50 GB of
+// scratch is ~40 B per input byte of a batch (the trie 16 B): 1 GiB batches (~40 GB of
 // HBM) because the parse has one walker per block and rate grows with walkers in flight
 // (256 MiB: 539 MB/s, 1 GiB: 1386 MB/s on rand)
 constexpr uint64_t kBatchBytes = 1024ull << 20;
@@ -705,7 +707,7 @@ int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_byte
     // blocks per batch: <= 1 GiB of input, and per-block scratch (trie, dense depth-1
     // table, group tables: large for tiny blocks) within a 64 GiB budget
     uint32_t cl2 = 10;
-    while ((1ull << cl2) < 2ull * block_bytes + 2) cl2++;
+    while ((1ull << cl2) < (uint64_t)block_bytes + 2) cl2++;
     const uint64_t per_block = (8ull << cl2) + (1ull << 18) + 64ull * std::max<uint32_t>(1024, block_bytes / 256 + 2) +
                                24ull * block_bytes + 4096;
     const uint64_t by_budget = std::max<uint64_t>(1, kScratchBudget / per_block);
