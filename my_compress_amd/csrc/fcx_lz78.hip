@@ -37,7 +37,8 @@
 namespace fcx78 {
 
 constexpr uint32_t kTileTok = 8192;   // tokens per pack tile (256 lanes x 32)
-constexpr uint32_t kSortCap = 8192;   // bitonic sort capacity (>= max group count 4097)
+constexpr uint32_t kSortCap = 8192;
+constexpr uint32_t kGroupLds = 4112;  // >= groups of a 1 MiB block (ceil((2^20 + 1) / 256))   // bitonic sort capacity (>= max group count 4097)
 
 struct Rec78 {
     uint32_t N, maxi, wcnt, G;
@@ -232,10 +233,18 @@ __global__ __launch_bounds__(1024) void k78_rank(Scratch S) {
 
 // token-parallel: rank -> group / in-group position, group counts
 __global__ __launch_bounds__(256) void k78_group(Scratch S) {
+    // group counts of the tile in LDS (G <= kGroupLds for blocks <= 1 MiB), flushed once
+    __shared__ uint32_t lc[kGroupLds];
     const uint32_t b = blockIdx.y, tid = threadIdx.x;
-    const uint32_t N = S.rec[b].N;
+    const Rec78 &R = S.rec[b];
+    const uint32_t N = R.N;
     const uint32_t t0 = blockIdx.x * kTileTok;
     if (t0 >= N) return;
+    const uint32_t G = R.G;
+    const bool lds = G <= kGroupLds;
+    if (lds)
+        for (uint32_t g = tid; g < G; g += 256) lc[g] = 0;
+    __syncthreads();
     const uint32_t *idx = S.idx + (uint64_t)b * S.B;
     const uint32_t *bm = S.bm + (uint64_t)b * S.bmw;
     const uint32_t *rb = S.rbase + (uint64_t)b * S.bmw;
@@ -248,8 +257,13 @@ __global__ __launch_bounds__(256) void k78_group(Scratch S) {
         const uint32_t r = rb[v >> 5] + __popc(bm[v >> 5] & ((1u << (v & 31)) - 1u));
         grp[t] = (uint16_t)(r >> 8);
         gp[t] = (uint8_t)(r & 255);
-        atomicAdd(&gc[r >> 8], 1u);
+        if (lds) atomicAdd(&lc[r >> 8], 1u);
+        else atomicAdd(&gc[r >> 8], 1u);
     }
+    __syncthreads();
+    if (lds)
+        for (uint32_t g = tid; g < G; g += 256)
+            if (lc[g]) atomicAdd(&gc[g], lc[g]);
 }
 
 // ---------------------------------------------------------------------------
