@@ -255,12 +255,36 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(kind, seed, block, threads=16, nblocks=32, nblocks_1t=4):
+def host_cpu_share():
+    """threads the CPU baseline may use: the CPUs this process may run on
+    (sched_getaffinity), capped by the cgroup CPU quota when one is set
+    (/sys/fs/cgroup/cpu.max); returns (threads, how it was determined)"""
+    aff = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            return min(aff, q), f"cgroup cpu.max quota {quota}/{period} = {q} CPUs (affinity {aff})"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < aff:
+        # the GPU box exports its per-GPU CPU share here (16) while affinity shows the whole host
+        return int(omp), f"OMP_NUM_THREADS={omp}: the host's per-GPU CPU share (affinity shows {aff})"
+    return aff, f"sched_getaffinity: {aff} CPUs (no cgroup quota)"
+
+
+def cpu_baseline(kind, seed, block, threads=None, nblocks=None, nblocks_1t=8):
     """the reference's block encoder (oracle/_ref, compiled from /root/reference) on
-    the first nblocks blocks of the same shard, `threads` host threads (the box's
-    CPU share), plus the first nblocks_1t blocks on one thread (the reference is
-    single-threaded)"""
+    the first nblocks blocks of the same shard, one host thread per CPU of this
+    process's share (host_cpu_share), plus the first nblocks_1t blocks on one thread
+    (the reference is single-threaded)"""
     import oracle
+
+    share, share_how = host_cpu_share()
+    threads = threads or share
+    nblocks = nblocks or min(256, 8 * threads)   # ~10-60 s of CPU work at 0.5-1 s per 1 MiB block
 
     R = oracle.ref()
     kind_used = "reference"
@@ -309,7 +333,7 @@ def cpu_baseline(kind, seed, block, threads=16, nblocks=32, nblocks_1t=4):
             "sample": f"first {nblocks} x {block // 1024} KiB blocks of the {kind} shard, {threads} threads "
                       f"({'reference my_compress_file_lz77 compiled in place' if R is not None else 'oracle port'})",
             "seconds": dt, "one_thread_MBps": one, "one_thread_sample": f"first {nblocks_1t} blocks, 1 thread",
-            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count()}
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "cores_source": share_how}
 
 
 def lz78_leg(dev, mib=1024, block=1 << 20, reps=2, ref_blocks=2):

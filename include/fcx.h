@@ -120,6 +120,11 @@ int fcx_compress_stream(fcx_ctx *ctx, fcx_read_fn read, fcx_write_fn write, void
 
 /* Enables per-kernel hipEvent timing of subsequent fcx_compress_shard calls. */
 int fcx_ctx_set_profiling(fcx_ctx *ctx, int enable);
+/* Testing: forces how the match kernel evaluates every tile of later calls —
+ * 0 auto (default), 1 bucket search (hash buckets, unknown positions via the run
+ * table / the stitch), 2 run table for whole tiles.  The output is identical in
+ * every mode; only the speed differs. */
+int fcx_ctx_set_match_mode(fcx_ctx *ctx, int mode);
 /* After a profiled call: number of stages, and stage i's name and device ms. */
 int fcx_ctx_stage_count(fcx_ctx *ctx);
 int fcx_ctx_stage(fcx_ctx *ctx, int i, const char **name, float *ms);

@@ -67,6 +67,7 @@ def lib():
     L.fcx_compress_host.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, c_u8p, ctypes.c_uint64,
                                     ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.fcx_ctx_set_match_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.fcx_ctx_stage_count.argtypes = [ctypes.c_void_p]
     L.fcx_ctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                 ctypes.POINTER(ctypes.c_float)]
@@ -193,6 +194,10 @@ class Context:
 
     def set_profiling(self, on: bool = True):
         _check(lib().fcx_ctx_set_profiling(self._h, 1 if on else 0), "fcx_ctx_set_profiling")
+
+    def set_match_mode(self, mode: int):
+        """testing: 0 auto, 1 bucket search, 2 run table for whole tiles (same output)"""
+        _check(lib().fcx_ctx_set_match_mode(self._h, mode), "fcx_ctx_set_match_mode")
 
     def stage_times(self):
         """[(stage name, device ms)] of the last profiled compress_shard"""

@@ -100,6 +100,7 @@ struct fcx_ctx {
     uint64_t *host_words = nullptr;    // pinned mirror
     // profiling
     bool profiling = false;
+    uint32_t match_mode = 0;   // k_match tile-mode bits (fcx_ctx_set_match_mode)
     hipEvent_t ev[kNumStages + 1] = {};
     bool have_times = false;
     bool timed = false;        // last call recorded events
@@ -246,6 +247,13 @@ int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
     return FCX_OK;
 }
 
+int fcx_ctx_set_match_mode(fcx_ctx *c, int mode) {
+    if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
+    if (mode < 0 || mode > 2) return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search) or 2 (run table)");
+    c->match_mode = mode == 1 ? 4u : mode == 2 ? 8u : 0u;   // k_match dbg bits 2 / 3: both keep the output exact
+    return FCX_OK;
+}
+
 int fcx_ctx_stage_count(fcx_ctx *c) { return c && c->timed ? kNumStages : 0; }
 
 int fcx_ctx_stage(fcx_ctx *c, int i, const char **name, float *ms) {
@@ -289,7 +297,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     HIP_TRY(hipMemsetAsync(c->s[2], 0, (uint64_t)L.sstride[2] * L.nblocks, st));
     HIP_TRY(hipMemsetAsync(c->s[3], 0, (uint64_t)L.sstride[3] * L.nblocks, st));
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
-    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, st);
+    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, st, c->match_mode);
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
     launch_parse(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->fp, c->tile_off, c->binfo, c->s[0], c->s[1], c->s[2],
                  c->s[3], st, ev ? ev + 3 : nullptr);

@@ -543,11 +543,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                   uint32_t *tinfo, hipStream_t st, uint32_t dbg_override) {
-    // FCX_MATCH_DBG (experiments only): bit0 skip searches, bit1 skip long extension (both: output invalid),
-    // bit2 never / bit3 always take the whole-tile run mode (output stays exact); bits 4-6 (phase exits)
-    // only through fcx_debug_match, which launches this kernel alone
-    static const uint32_t env = getenv("FCX_MATCH_DBG") ? (uint32_t)atoi(getenv("FCX_MATCH_DBG")) & 15u : 0u;
-    const uint32_t dbg = dbg_override != ~0u ? dbg_override : env;
+    // dbg bits exist only for fcx_debug_match (development; launches this kernel alone on
+    // scratch the caller discards): bit0 skip searches, bit1 skip long extension, bit2 never /
+    // bit3 always take the whole-tile run mode, bits 4-6 phase exits.  The product path
+    // (fcx_compress_shard) always passes 0; nothing is read from the environment.
+    const uint32_t dbg = dbg_override != ~0u ? dbg_override : 0u;
     const uint32_t grid = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, dbg);
 }

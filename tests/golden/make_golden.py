@@ -33,6 +33,8 @@ REF.ref_golomb_encode.restype = ctypes.c_uint32
 REF.ref_combine_bits.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_void_p]
 REF.ref_huffman_tree.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
 REF.ref_huffman_tree.restype = ctypes.c_uint32
+REF.ref_decompress_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+REF.ref_decompress_block.restype = ctypes.c_int64
 REF.ref_set_quiet(1)
 
 
@@ -45,6 +47,22 @@ def ref_file(data: bytes, block: int) -> bytes:
         blk = data[off:off + block]
         n = REF.ref_compress_block(blk, len(blk), ob)
         out += struct.pack("<I", n) + ob.raw[:n]
+    return bytes(out)
+
+
+def ref_decode_file(blob: bytes) -> bytes:
+    """main()'s decompress loop (my_compress.cpp:4160-4204) around the reference
+    block decoder my_decompress_file_lz77 (2255-2393): the decoded bytes of every
+    record, concatenated, quirks included (single-symbol sub-streams decode as
+    zeros 930-984; a match token past pCnt stops the block, 2336-2339)."""
+    nblk = struct.unpack_from("<H", blob, 8)[0]
+    off, out = 10, bytearray()
+    ob = ctypes.create_string_buffer((1 << 20) + 4096)
+    for _ in range(nblk):
+        (n,) = struct.unpack_from("<I", blob, off)
+        got = REF.ref_decompress_block(blob[off + 4:off + 4 + n], n, ob, len(ob))
+        out += ob.raw[:got]
+        off += 4 + n
     return bytes(out)
 
 
@@ -68,6 +86,8 @@ def main():
         out = ref_file(data, spec["block"])
         rec = dict(spec)
         rec.update(in_sha256=sha(data), in_bytes=len(data), out_bytes=len(out), out_sha256=sha(out))
+        dec = ref_decode_file(out)
+        rec.update(dec_bytes=len(dec), dec_sha256=sha(dec), dec_is_input=dec == data)
         if len(out) <= 4096:
             rec["out_hex"] = out.hex()
         cases.append(rec)

@@ -117,6 +117,18 @@ def golden_specs():
         {"type": "gen", "kind": "text", "seed": 22, "n": 100000}]})
     S.append({"name": "text_plus_partial", "type": "concat", "block": 262144, "parts": [
         {"type": "gen", "kind": "text", "seed": 5, "n": MiB + 12345}]})
+    # decoder quirks (my_compress.cpp:2255-2393): an all-literal block whose flag bytes
+    # are all 0xFF has a one-symbol flags stream, which the reference decodes as zeros,
+    # so its first "match" token finds pCnt exhausted and the block stops empty
+    # (2336-2339); 4100 bytes leave a partial last flag byte (two symbols, decodes fine)
+    S.append(_g("rand", 31, 4096, 4096, name="quirk_rand4k_empty"))
+    S.append(_g("rand", 32, 4 * 4096, 4096, name="quirk_rand4k_x4"))
+    S.append(_g("rand", 33, 4100, 8192, name="quirk_rand4100"))
+    S.append({"name": "quirk_text_rand_text", "type": "concat", "block": 4096, "parts": [
+        {"type": "gen", "kind": "text", "seed": 34, "n": 6000},
+        {"type": "gen", "kind": "rand", "seed": 35, "n": 8192},
+        {"type": "gen", "kind": "text", "seed": 36, "n": 6000}]})
+    S.append({"name": "quirk_two_symbols", "type": "repeat", "hex": b"AB".hex(), "count": 3000, "block": 1000})
     return S
 
 
@@ -153,3 +165,34 @@ SURVEY_DIGESTS = {
                      "in": "2a96181ea4cf7c0c9cfff49677640efe0a5a0b12ee5d0379f2bdf06d9c41f29d",
                      "bytes": 1091294206, "out": "ee962534628bf6b2f79c51a44a65ac0845945e2fe9225e5be8f99f288912a69d"},
 }
+
+# BASELINE config 4 (8 GiB rand seed 4, 1 MiB blocks) split over 8 ranks: rank r
+# compresses bytes [r GiB, (r+1) GiB) of the one stream into its segment of
+# [u32 len][payload] records (no header).  Sizes and sha256 prefixes of the
+# reference's segments; the whole file is
+# 10 + sum(bytes) = 8,730,352,595 B with sha256 8f1cae2f... (header total wraps to 0).
+C4_SEGMENTS = [
+    (1091294196, "6e3350797c82335d"),
+    (1091294015, "baccd8ba445a9881"),
+    (1091294276, "9b42660291458d16"),
+    (1091294478, "df0203068ca7daa3"),
+    (1091294029, "7330de83672cbb7d"),
+    (1091293907, "d31a6f66f351bab0"),
+    (1091293647, "3663bdd18b38bc7f"),
+    (1091294037, "018665b30a10d61d"),
+]
+C4_FILE = {"bytes": 8730352595, "out": "8f1cae2fa6fbc3b597bd90b83fd0998ffeb7d827e199a9f6aa3c25fea587656c"}
+
+
+def rand_stream_into(seed: int, offset: int, ptr: int, n: int) -> None:
+    """bytes [offset, offset + n) of the rand stream of `seed` (glibc rand()%256),
+    via the generator's O(log offset) jump-ahead: rank shards of one global input"""
+    G = gen_lib()
+    G.fcxgen_skip.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    h = G.fcxgen_create(GEN_KIND["rand"], seed)
+    try:
+        G.fcxgen_skip(h, offset)
+        G.fcxgen_fill(h, ctypes.c_void_p(ptr), n)
+    finally:
+        G.fcxgen_destroy(h)
+

@@ -45,6 +45,22 @@ def test_cli_decompresses_reference_streams(tmp_path, golden):
         assert (tmp_path / "plain").read_bytes() == data
 
 
+def test_cli_decoder_quirks_match_reference_decoder(tmp_path, golden):
+    """files whose reference decode is not the input (one-symbol sub-streams decode
+    as zeros, my_compress.cpp:930-984; early stop at 2336-2339): the CLI writes the
+    reference decoder's bytes and, like main() (4198-4201), reports FAIL on the size"""
+    for case in golden["cases"]:
+        if case["dec_is_input"] or case["in_bytes"] > 1 << 20:
+            continue
+        blob = oracle.compress_file(inputs.make(case), case["block"])
+        (tmp_path / "in.fcx").write_bytes(blob)
+        r = run(["-i", "in.fcx", "-o", "plain"], tmp_path)
+        out = (tmp_path / "plain").read_bytes()
+        assert hashlib.sha256(out).hexdigest() == case["dec_sha256"], case["name"]
+        size_ok = case["dec_bytes"] == case["in_bytes"]
+        assert ("SUCCESS" in r.stdout) == size_ok, (case["name"], r.stdout)
+
+
 def test_cli_rejects_foreign_stream(tmp_path):
     (tmp_path / "junk").write_bytes(b"NOTFCX" * 10)
     assert run(["-i", "junk", "-o", "x"], tmp_path).returncode != 0

@@ -4,6 +4,7 @@ my_compress.cpp:2255-2393, pinned in test_oracle.py) on the reference's own
 streams (golden.json inputs, encoded by the oracle = the reference's bytes), plus
 round trips of the GPU encoder at block sizes 1 B .. 1 MiB and at full size.
 Bar: bit-exact, including the reference's single-symbol and early-stop quirks."""
+import hashlib
 import random
 
 import pytest
@@ -23,15 +24,38 @@ def dctx(cuda):
 
 
 def test_golden_streams(golden, dctx):
+    """every golden case: the GPU decoder's bytes = the reference decoder's
+    (golden.json dec_sha256, made by my_decompress_file_lz77 compiled in place)"""
     bad = []
     for case in golden["cases"]:
         data = inputs.make(case)
-        blob = oracle.compress_file(data, case["block"])
-        want = oracle.decompress_file(blob, len(data) + 16)
+        blob = oracle.compress_file(data, case["block"])   # the reference's bytes (pinned in test_oracle)
         got = dctx.decompress_host(blob, len(data) + 16)
-        if got != want:
+        if len(got) != case["dec_bytes"] or hashlib.sha256(got).hexdigest() != case["dec_sha256"]:
             bad.append(case["name"])
     assert not bad, f"GPU decoder differs from the reference decoder on {bad}"
+
+
+def test_golden_streams_device_api(golden, dctx, cuda):
+    """the same through fcx_decompress_shard on device-resident records"""
+    import struct
+
+    import torch
+
+    bad = []
+    for case in golden["cases"]:
+        if case["in_bytes"] > 1 << 20:
+            continue
+        blob = oracle.compress_file(inputs.make(case), case["block"])
+        nblk = struct.unpack_from("<H", blob, 8)[0]
+        d_rec = torch.frombuffer(bytearray(blob[10:] or b"\0"), dtype=torch.uint8).to(cuda)
+        d_out = torch.zeros(case["in_bytes"] + 64, dtype=torch.uint8, device=cuda)
+        got = dctx.decompress_shard(d_rec.data_ptr(), len(blob) - 10, nblk, d_out.data_ptr(), d_out.numel(),
+                                    torch.cuda.current_stream().cuda_stream)
+        out = d_out[:got].cpu().numpy().tobytes()
+        if got != case["dec_bytes"] or hashlib.sha256(out).hexdigest() != case["dec_sha256"]:
+            bad.append(case["name"])
+    assert not bad, f"fcx_decompress_shard differs from the reference decoder on {bad}"
 
 
 def test_single_symbol_stream_decodes_as_zeros(dctx):

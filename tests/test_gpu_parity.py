@@ -25,10 +25,11 @@ def gpu_compress(cuda):
 
     ctxs = {}
 
-    def run(data: bytes, block: int) -> bytes:
-        if block not in ctxs:
-            ctxs[block] = mc.Context(0, block, max(len(data), block))
-        ctx = ctxs[block]
+    def run(data: bytes, block: int, mode: int = 0) -> bytes:
+        if (block, mode) not in ctxs:
+            ctxs[(block, mode)] = mc.Context(0, block, max(len(data), block))
+            ctxs[(block, mode)].set_match_mode(mode)
+        ctx = ctxs[(block, mode)]
         if not data:
             return mc.write_header(0, 0)
         d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
@@ -57,6 +58,20 @@ def test_golden_cases_bit_exact(golden, gpu_compress):
         if hashlib.sha256(out).hexdigest() != case["out_sha256"]:
             bad.append((case["name"], len(out), case["out_bytes"]))
     assert not bad, f"GPU output differs from the reference on {bad}"
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_golden_cases_forced_match_mode(golden, gpu_compress, mode):
+    """every tile through one evaluation path of k_match (1: hash buckets + run table
+    for the unknowns, 2: run table for whole tiles): the output must not change"""
+    bad = []
+    for case in _cases(golden):
+        if case["in_bytes"] > 1 << 20:
+            continue
+        out = gpu_compress(inputs.make(case), case["block"], mode)
+        if hashlib.sha256(out).hexdigest() != case["out_sha256"]:
+            bad.append(case["name"])
+    assert not bad, f"match mode {mode}: GPU output differs from the reference on {bad}"
 
 
 def test_small_hex_fixtures(golden, gpu_compress):
@@ -146,3 +161,40 @@ def test_full_size_digests(name, cuda):
     h.update(memoryview(out_host.numpy()))
     assert got + 10 == cfg["bytes"]
     assert h.hexdigest() == cfg["out"]
+
+
+@pytest.mark.slow
+def test_cfg4_rank_segments(cuda):
+    """BASELINE config 4 (8 GiB rand seed 4 over 8 GPUs) on one GPU, rank by rank:
+    rank r's 1 GiB shard is bytes [r GiB, (r+1) GiB) of the one stream, and its
+    segment must equal the reference's (size + sha256 prefix, SURVEY.md B.3;
+    main()'s framing my_compress.cpp:4090-4122).  The concatenation of the eight
+    segments behind the 10-byte header must be the reference's 8 GiB file."""
+    import torch
+
+    n, block = 1 << 30, 1 << 20
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    d_in = torch.empty(n, dtype=torch.uint8, device=cuda)
+    cap = mc.shard_bound(n, block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+    ctx = mc.Context(0, block, n)
+    whole = hashlib.sha256(mc.write_header(8 * n, 8 * n // block))
+    total = 10
+    bad = []
+    try:
+        for r, (want_bytes, want_prefix) in enumerate(inputs.C4_SEGMENTS):
+            inputs.rand_stream_into(4, r * n, host.data_ptr(), n)
+            d_in.copy_(host)
+            got = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap,
+                                     torch.cuda.current_stream().cuda_stream)
+            seg = d_out[:got].cpu().numpy()
+            h = hashlib.sha256(memoryview(seg)).hexdigest()
+            whole.update(memoryview(seg))
+            total += got
+            if got != want_bytes or h[:16] != want_prefix:
+                bad.append((r, got, want_bytes, h[:16], want_prefix))
+    finally:
+        ctx.close()
+    assert not bad, f"config-4 rank segments differ from the reference: {bad}"
+    assert total == inputs.C4_FILE["bytes"]
+    assert whole.hexdigest() == inputs.C4_FILE["out"]

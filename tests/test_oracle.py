@@ -103,6 +103,21 @@ def test_oracle_matches_reference_outputs(golden):
             assert out.hex() == case["out_hex"]
 
 
+def test_oracle_decoder_matches_reference_decoder(golden):
+    """the oracle's decoder against my_decompress_file_lz77 (:2255-2393) itself:
+    golden.json holds the reference decoder's output for every case (quirks
+    included: one-symbol sub-streams decode as zeros, 930-984; a match token past
+    pCnt stops the block, 2336-2339)"""
+    quirky = 0
+    for case in golden["cases"]:
+        blob = oracle.compress_file(inputs.make(case), case["block"])   # = the reference's bytes (test above)
+        dec = oracle.decompress_file(blob, case["in_bytes"] + 16)
+        assert len(dec) == case["dec_bytes"], case["name"]
+        assert hashlib.sha256(dec).hexdigest() == case["dec_sha256"], case["name"]
+        quirky += not case["dec_is_input"]
+    assert quirky >= 5   # the fixture really exercises the quirks
+
+
 def test_sunday_and_exhaustive_finders_agree():
     for seed in range(6):
         data = inputs.mosaic(seed, 40000)

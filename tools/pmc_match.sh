@@ -7,6 +7,6 @@ for kind in ${KINDS:-text rand}; do
   case $kind in text) seed=3;; rand) seed=4;; runs) seed=5;; *) seed=0;; esac
   for set in A B; do
     eval "C=\$$set"
-    timeout -k 10 200 rocprofv3 --kernel-trace --pmc $C -d $R/gpurun_out/pmc_${kind}_$set -o run --output-format csv -- python3 $R/tools/devbench.py --kind $kind --seed $seed --mib 256 --reps 1 > $R/gpurun_out/pmc_${kind}_$set.log 2>&1 || exit 1
+    timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $C -d $R/gpurun_out/pmc_${kind}_$set -o run --output-format csv -- python3 $R/tools/devbench.py --kind $kind --seed $seed --mib 256 --reps 1 > $R/gpurun_out/pmc_${kind}_$set.log 2>&1 || exit 1
   done
 done
