@@ -2,20 +2,26 @@
 """bench.py — compress throughput of the MI355X FCX7 LZ77 + Huffman path.
 
 Metric (BASELINE.json): compress MB/s on 1 GB synthetic bytes at 1/2/4/8 MI355X;
-% HBM roofline.  One process per GPU (torchrun for N > 1).  A "step" compresses
-the rank's whole device-resident shard (1 GiB = 1024 x 1 MiB blocks by default)
-into [u32 len][payload]... in HBM.  Shards are independent block ranges, so the
-data path has no collective (scaling: weak); the RCCL all-gather that
-concatenates the per-rank segments is timed after the timed region as its own
-stage ("concat").
+% HBM roofline.  One process per GPU (torchrun for N > 1), RCCL over xGMI.
 
-Default workload: rand = glibc rand()%256 seed 4, rank r = bytes [r GiB,
-(r+1) GiB) of that one stream (BASELINE config 4 sharding; N=1 is SURVEY's
-HL-rand, whose output digest is checked).  The text leg (seed 3 + rank; N=1 is
-HL-text) is measured in the same run and reported under "text".
+Headline (default, `scaling: strong`): ONE 1 GiB input (--global-mib) split into
+contiguous block ranges over the N ranks.  A timed step is the
+whole job: every rank compresses its device-resident shard into [u32 len][payload]
+records in HBM, the segment sizes are all-gathered, and the segments are
+concatenated in rank order into one contiguous stream on rank 0 (--concat gather:
+grouped point-to-point receives over all xGMI links; `allgather`: every rank gets
+the stream, one broadcast per source rank).  `value` = global input bytes x K /
+the max-over-ranks time of K such steps.  At N=1 there is nothing to concatenate.
+The compress-only rate (no exchange) is reported beside it.  The assembled stream
+is checked against the reference's SHA-256 (HL-rand / HL-text / C3 / C5 digests,
+SURVEY.md §8(c)) at every N.
+
+Extra leg `weak` (N > 1; BASELINE config 4): rank r compresses bytes [r GiB,
+(r+1) GiB) of the seed-4 rand stream, each rank's segment checked against the
+reference's, the N segments gathered to rank 0.
 
     python bench.py                      # N=1, defaults
-    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         --master-port 29500 bench.py --gpus 8
 """
 import argparse
@@ -33,114 +39,224 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 METRIC = "compress MB/s on 1 GB synthetic bytes at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-HL_DIGEST = {  # reference output digests for the N=1 shards
-    ("rand", 4, 1 << 30, 1 << 20): ("ee962534628bf6b2f79c51a44a65ac0845945e2fe9225e5be8f99f288912a69d", 1091294206),
-    ("text", 3, 1 << 30, 1 << 20): ("132a36b9d2592f8c37a82b51f545ddb67acec53fa1a31b7f1f6a04617a01a3d1", 624801500),
-    ("text", 3, 1 << 30, 1 << 18): ("20219e60c2e9aef6659801fbfc53c6873ec811686eedcb45c0896fc5547d63d0", 630008807),
-    ("zeros", 0, 1 << 30, 1 << 20): ("533fd45fbaa861a6060e9a5beac177cc0b64db691fc602a1e0e1e188afa5f912", 7521290),
-    ("runs", 5, 1 << 30, 1 << 20): ("4fced94fd4725ba3b1031dec67d63e1295b95ae08cc1cf0e34c84769f5313d26", 42548682),
+GiB = 1 << 30
+HL_DIGEST = {  # reference output digests of whole files: (kind, seed, bytes, block)
+    ("rand", 4, GiB, 1 << 20): ("ee962534628bf6b2f79c51a44a65ac0845945e2fe9225e5be8f99f288912a69d", 1091294206),
+    ("text", 3, GiB, 1 << 20): ("132a36b9d2592f8c37a82b51f545ddb67acec53fa1a31b7f1f6a04617a01a3d1", 624801500),
+    ("text", 3, GiB, 1 << 18): ("20219e60c2e9aef6659801fbfc53c6873ec811686eedcb45c0896fc5547d63d0", 630008807),
+    ("zeros", 0, GiB, 1 << 20): ("533fd45fbaa861a6060e9a5beac177cc0b64db691fc602a1e0e1e188afa5f912", 7521290),
+    ("runs", 5, GiB, 1 << 20): ("4fced94fd4725ba3b1031dec67d63e1295b95ae08cc1cf0e34c84769f5313d26", 42548682),
+    ("rand", 2, 64 << 20, 1 << 16): ("3b6853f2cf570b7a35c469efff62c15e0290b04ede45f6b47a97afc82c1878a5", 68819158),
 }
-# extra legs measured after the main one: name -> (kind, seed, block bytes); BASELINE configs 3 and 5
-LEGS = {"text": ("text", 3, 1 << 20), "c3": ("text", 3, 1 << 18), "zeros": ("zeros", 0, 1 << 20),
-        "runs": ("runs", 5, 1 << 20)}
+SEEDS = {"rand": 4, "text": 3, "runs": 5, "zeros": 0, "dna": 6}
+# extra legs after the main one: name -> (kind, block bytes); BASELINE configs 3 and 5, plus
+# "dna" (rand()%4 bytes: dense 3-byte buckets, the lazy-evaluation path)
+LEGS = {"text": ("text", 1 << 20), "c3": ("text", 1 << 18), "zeros": ("zeros", 1 << 20),
+        "runs": ("runs", 1 << 20), "dna": ("dna", 1 << 20)}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_shard(kind, seed, rank, n):
-    """pinned host tensor with rank's shard of the synthetic stream"""
+def make_input(kind, seed, lo, hi, pinned=True):
+    """bytes [lo, hi) of the synthetic stream `kind`/`seed` in a
+    (pinned) host tensor.  rand jumps ahead in O(log lo); the other streams are
+    generated from their start and sliced."""
     import torch
 
     import inputs
 
-    G = inputs.gen_lib()
-    G.fcxgen_skip.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    host = torch.empty(n, dtype=torch.uint8).pin_memory()
-    if kind == "rand":
-        h = G.fcxgen_create(inputs.GEN_KIND["rand"], seed)
-        G.fcxgen_skip(h, rank * n)   # one stream, rank r starts at byte r*n
-        G.fcxgen_fill(h, host.data_ptr(), n)
-        G.fcxgen_destroy(h)
+    n = hi - lo
+    host = torch.empty(max(n, 1), dtype=torch.uint8)
+    if pinned:
+        host = host.pin_memory()
+    if kind in ("rand", "dna"):
+        inputs.rand_stream_into(seed, lo, host.data_ptr(), n, kind)
+    elif kind == "zeros" or lo == 0:
+        inputs.generate_into(kind, seed, host.data_ptr(), n)
     else:
-        inputs.generate_into(kind, seed + rank, host.data_ptr(), n)
+        whole = torch.empty(hi, dtype=torch.uint8)
+        inputs.generate_into(kind, seed, whole.data_ptr(), hi)
+        host[:n].copy_(whole[lo:hi])
+        del whole
     return host
 
 
-def run_leg(kind, seed, args, rank, world, dev, dist, profile_stages, block=None):
+def max_over_ranks(dt, dist, dev):
     import torch
 
-    import my_compress_amd as mc
+    if not dist:
+        return dt
+    tt = torch.tensor([dt], dtype=torch.float64)
+    if dist.get_backend() != "gloo":
+        tt = tt.to(dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
 
-    n = args.mib << 20
-    block = block or args.block
-    t = time.time()
-    host = make_shard(kind, seed, rank, n)
-    gen_s = time.time() - t
-    d_in = host.to(dev)
-    host_path = None
-    if world == 1 and args.host_path and kind == args.kind:
-        host_path = host_leg(host, n, block)
-    del host
-    cap = mc.shard_bound(n, block)
-    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
-    ctx = mc.Context(dev.index, block, n)
-    stream = torch.cuda.current_stream(dev)
-    sid = stream.cuda_stream
-    out_len = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid)  # validates the call
-    for _ in range(args.warmup):
-        ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid, sync=False)
-    ctx.set_profiling(profile_stages)
-    stage_sum = {}
+
+def timed(fn, steps, dist, dev):
+    """barrier + synchronize on both sides of `steps` calls; max over ranks"""
+    import torch
+
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid, sync=False)
-        if profile_stages:
-            for name, ms in ctx.stage_times():   # waits for this step's last event
-                stage_sum[name] = stage_sum.get(name, 0.0) + ms
+    for _ in range(steps):
+        fn()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
-    dt = time.perf_counter() - t0
+    return max_over_ranks(time.perf_counter() - t0, dist, dev)
+
+
+def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, scaling="strong", main_leg=False):
+    """one leg.  strong: the global input of args.global_mib MiB split over the ranks;
+    weak: args.mib MiB per rank (rand: rank r = bytes [r*shard, (r+1)*shard) of one stream)."""
+    import torch
+
+    import my_compress_amd as mc
+    from my_compress_amd import dist as fdist
+
+    if scaling == "strong":
+        n_global = args.global_mib << 20
+        lo, hi = fdist.byte_range(n_global, block, rank, world)
+    else:
+        per = args.mib << 20
+        n_global = per * world
+        lo, hi = rank * per, (rank + 1) * per
+    n = hi - lo
+    t = time.time()
+    if scaling == "weak" and kind != "rand":
+        host = make_input(kind, seed + rank, 0, n)   # independent per-rank streams
+    else:
+        host = make_input(kind, seed, lo, hi)
+    gen_s = time.time() - t
+    d_in = host.to(dev)
+    host_path = None
+    if world == 1 and args.host_path and main_leg:
+        host_path = host_leg(host, n, block)
+    del host
+    concat = args.concat if world > 1 else "none"
+    # gather: rank 0's compress output buffer is also the file buffer (its segment sits at offset 0)
+    cap = mc.shard_bound(n_global if (concat == "gather" and rank == 0) else n, block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    whole = None
+    if concat == "allgather":
+        whole = torch.empty(mc.shard_bound(n_global, block), dtype=torch.uint8, device=dev)
+    ctx = mc.Context(dev.index, block, max(n, block))
+    sid = torch.cuda.current_stream(dev).cuda_stream
+    state = {}
+
+    def compress():
+        if n:
+            ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid, sync=False)
+
+    def step():   # the whole job: compress, sizes, concatenation in rank order
+        compress()
+        seg_len = ctx.read_out_len() if n else 0
+        if concat == "none":
+            state["total"] = seg_len
+            return
+        sizes, offs = fdist.exchange_sizes(seg_len, dist, dev if dist.get_backend() != "gloo" else "cpu")
+        seg = d_out[:seg_len]
+        if dist.get_backend() == "gloo":   # rehearsal without RCCL: the segments travel through host memory
+            hbuf = torch.empty(sum(sizes) + 1, dtype=torch.uint8)
+            hseg = seg.cpu()
+            if concat == "gather":
+                fdist.gather_segments(hseg, hbuf, sizes, offs, dist, 0)
+            else:
+                fdist.allgather_segments(hseg, hbuf, sizes, offs, dist)
+            if rank == 0:
+                (d_out if concat == "gather" else whole)[:sum(sizes)].copy_(hbuf[:sum(sizes)])
+        elif concat == "gather":
+            fdist.gather_segments(seg, d_out, sizes, offs, dist, 0)
+        else:
+            fdist.allgather_segments(seg, whole, sizes, offs, dist)
+        state["total"], state["seg"] = sum(sizes), seg_len
+
+    step()   # validates the call, creates the communicators
+    for _ in range(args.warmup):
+        step()
+    # compress only (device-resident, no exchange), per-kernel hipEvent times on the side
+    ctx.set_profiling(profile_stages)
+    stage_sum = {}
+
+    def compress_profiled():
+        compress()
+        if profile_stages and n:
+            for name, ms in ctx.stage_times():   # waits for this step's last event
+                stage_sum[name] = stage_sum.get(name, 0.0) + ms
+
+    dt_c = timed(compress_profiled, args.steps, dist, dev)
     ctx.set_profiling(False)
-    if dist:
-        tt = torch.tensor([dt], dtype=torch.float64)
-        if dist.get_backend() != "gloo":
-            tt = tt.to(dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    out_len = ctx.read_out_len()   # segment size of the timed steps (device word)
+    seg_len = ctx.read_out_len() if n else 0
+    # the whole job, K steps
+    dt = timed(step, args.steps, dist, dev) if concat != "none" else dt_c
+    total = state.get("total", seg_len)
     res = {
-        "kind": kind, "block_bytes": block, "bytes_per_gpu": n, "out_bytes": out_len, "ratio": out_len / n,
-        "seconds": dt, "ms_per_step": dt / args.steps * 1e3,
-        "value": world * n * args.steps / dt / 1e6, "gen_s": gen_s,
-        "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
-        "host_path": host_path,
+        "kind": kind, "block_bytes": block, "scaling": scaling, "global_bytes": n_global, "bytes_this_rank": n,
+        "out_bytes": total, "ratio": total / max(n_global, 1), "concat": concat,
+        "seconds": dt, "ms_per_step": dt / args.steps * 1e3, "value": n_global * args.steps / dt / 1e6,
+        "compress_only": {"value": n_global * args.steps / dt_c / 1e6, "ms_per_step": dt_c / args.steps * 1e3,
+                          "note": "device-resident compress of every rank's shard, no exchange (max over ranks)"},
+        "gen_s": gen_s, "stages_ms": {k: v / args.steps for k, v in stage_sum.items()}, "host_path": host_path,
+        "seg_bytes_rank0": seg_len,
     }
-    stats = ctx.stats()
+    if concat != "none":
+        res["concat_ms_per_step"] = res["ms_per_step"] - res["compress_only"]["ms_per_step"]
+    stats = ctx.stats() if n else {"tokens": 0, "matches": 0, "lazy_evals": 0, "lazy_tiles": 0}
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
-    key = (kind, seed, n, block)
-    if rank == 0 and world == 1 and key in HL_DIGEST and not args.no_verify:
-        import my_compress_amd as mc2
-
-        h = hashlib.sha256(mc2.write_header(n, (n + block - 1) // block))
-        h.update(memoryview(d_out[:out_len].cpu().numpy()))
-        want_sha, want_bytes = HL_DIGEST[key]
-        res["bit_exact_vs_reference"] = h.hexdigest() == want_sha and out_len + 10 == want_bytes
-    if not args.no_decode:
-        res["decode"] = decode_leg(d_out, out_len, n, block, d_in, args, dev, dist, world)
-    concat = None
-    if dist and world > 1 and args.concat == "allgather":
-        concat = allgather_concat(d_out, out_len, world, dev, dist)
+    if not args.no_verify:
+        res.update(verify(kind, seed, block, n_global, scaling, rank, world, dev, dist, d_out, whole, concat,
+                          seg_len, total))
+    if not args.no_decode and (main_leg or world == 1):
+        res["decode"] = decode_leg(d_out, seg_len, n, block, d_in, args, dev, dist, world)
     ctx.close()
-    del d_in, d_out
+    del d_in, d_out, whole
     torch.cuda.empty_cache()
-    return res, concat
+    return res
+
+
+def verify(kind, seed, block, n_global, scaling, rank, world, dev, dist, d_out, whole, concat, seg_len, total):
+    """digest of the assembled stream (rank 0) against the reference's; weak rand:
+    every rank's segment against SURVEY.md B.3"""
+    import torch
+
+    import inputs
+    import my_compress_amd as mc
+
+    out = {}
+    if scaling == "weak" and kind == "rand" and seed == 4 and n_global // world == GiB:
+        ok = 0
+        if rank < len(inputs.C4_SEGMENTS):
+            want_bytes, want_prefix = inputs.C4_SEGMENTS[rank]
+            h = hashlib.sha256(memoryview(d_out[:seg_len].cpu().numpy())).hexdigest()
+            ok = int(seg_len == want_bytes and h[:16] == want_prefix)
+        flags = torch.tensor([ok], dtype=torch.int64)
+        if dist:
+            if dist.get_backend() != "gloo":
+                flags = flags.to(dev)
+            allf = [torch.zeros_like(flags) for _ in range(world)]
+            dist.all_gather(allf, flags)
+            oks = [int(x.item()) for x in allf]
+        else:
+            oks = [ok]
+        out["rank_segments_bit_exact"] = oks
+        out["bit_exact_vs_reference"] = all(oks)
+        return out
+    key = (kind, seed, n_global, block)
+    if key not in HL_DIGEST or rank != 0:
+        return out
+    stream = d_out if concat in ("none", "gather") else whole
+    h = hashlib.sha256(mc.write_header(n_global, (n_global + block - 1) // block))
+    h.update(memoryview(stream[:total].cpu().numpy()))
+    want_sha, want_bytes = HL_DIGEST[key]
+    out["bit_exact_vs_reference"] = h.hexdigest() == want_sha and total + 10 == want_bytes
+    out["checked"] = "sha256 of header + assembled stream on rank 0 vs the reference's file (SURVEY.md B.4)"
+    return out
 
 
 def host_leg(host, n, block, reps=3):
@@ -213,35 +329,6 @@ def decode_leg(d_rec, rec_len, n, block, d_in, args, dev, dist, world):
     return {"value": world * n * args.steps / dt / 1e6, "unit": "MB/s (decoded bytes)",
             "ms_per_step": dt / args.steps * 1e3, "round_trip_exact": ok,
             "stages_ms": {k: v / args.steps for k, v in stage_sum.items()}}
-
-
-def allgather_concat(d_out, seg_len, world, dev, dist):
-    """RCCL all-gather of the per-rank segments (my_compress_amd.dist): sizes,
-    then segments padded to the largest, assembled in rank order on every rank.
-    With the gloo backend (rehearsal) the segments travel through host memory."""
-    import torch
-
-    from my_compress_amd import dist as fdist
-
-    on_host = dist.get_backend() == "gloo"
-    dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    seg = d_out[:seg_len]
-    if on_host:
-        seg = seg.cpu()
-    whole = fdist.concat_segments(seg, dist)
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    tt = torch.tensor([dt], dtype=torch.float64)
-    if not on_host:
-        tt = tt.to(dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    dt = float(tt.item())
-    total = int(whole.numel())
-    del whole
-    return {"kind": "allgather" + ("(gloo,host)" if on_host else "(rccl)"), "ms": dt * 1e3, "bytes": total,
-            "GBps_per_rank_recv": (total - seg_len) / dt / 1e9}
 
 
 def cpu_model():
@@ -403,13 +490,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--kind", default="rand", choices=["rand", "text", "runs", "zeros"])
-    ap.add_argument("--mib", type=int, default=1024, help="MiB per GPU")
+    ap.add_argument("--kind", default="rand", choices=["rand", "text", "runs", "zeros", "dna"])
+    ap.add_argument("--global-mib", type=int, default=1024, help="headline input size, split over the ranks")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="main leg: strong = --global-mib split N ways (default), weak = --mib per rank")
+    ap.add_argument("--mib", type=int, default=1024, help="MiB per rank for weak scaling (the weak leg)")
     ap.add_argument("--block", type=int, default=1 << 20)
     ap.add_argument("--no-text", action="store_true", help="skip every extra leg")
-    ap.add_argument("--legs", default="text,c3,zeros,runs",
+    ap.add_argument("--legs", default="text,c3,zeros,runs,dna",
                     help="extra legs after the main one (comma list of " + ",".join(LEGS) + ")")
-    ap.add_argument("--concat", default="allgather", choices=["allgather", "none"])
+    ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling (config 4) leg at N > 1")
+    ap.add_argument("--concat", default="gather", choices=["gather", "allgather", "none"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the GPU decoder timing")
@@ -437,63 +528,77 @@ def main():
         else:
             dist_.init_process_group("gloo")
         dist = dist_
-    seeds = {"rand": 4, "text": 3, "runs": 5, "zeros": 0}
-    main_res, concat = run_leg(args.kind, seeds[args.kind], args, rank, world, dev, dist, True)
+    main_res = run_leg(args.kind, SEEDS[args.kind], args.block, args, rank, world, dev, dist, True,
+                       scaling=args.scaling, main_leg=True)
     legs = {}
     for name in ([] if args.no_text else [x for x in args.legs.split(",") if x]):
-        kind, seed, block = LEGS[name]
+        kind, block = LEGS[name]
         if kind == args.kind and block == args.block:
             continue
-        legs[name], _ = run_leg(kind, seed, args, rank, world, dev, dist, True, block=block)
+        legs[name] = run_leg(kind, SEEDS[kind], block, args, rank, world, dev, dist, True)
+    weak = None
+    if world > 1 and not args.no_weak and args.scaling == "strong":
+        weak = run_leg("rand", 4, 1 << 20, args, rank, world, dev, dist, False, scaling="weak")
 
     if rank == 0:
         stages = {k: v for k, v in main_res["stages_ms"].items() if k != "memset"}
         dom = max(stages, key=stages.get) if stages else None
-        n = main_res["bytes_per_gpu"]
-        alg = n + main_res["out_bytes"]          # 1 + r bytes per input byte
+        n = main_res["bytes_this_rank"]
+        alg = n + main_res["seg_bytes_rank0"]     # 1 + r bytes per input byte, this rank's launch
         achieved = alg / (stages[dom] * 1e-3) / 1e9 if dom else None
         pmc = load_pmc(args.pmc)
         traffic = None
         key = f"{args.kind}:{dom}"
-        if key in pmc:
-            traffic = pmc[key].get("hbm_bytes_per_launch")
+        if key in pmc:   # PMC passes ran on a whole 1 GiB shard; scale to this rank's launch
+            t_in = pmc[key].get("input_bytes", GiB)
+            traffic = pmc[key].get("hbm_bytes_per_launch") * n / t_in
         roof = {"bound": "hbm", "kernel": f"k_{dom}" if dom else None, "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "alg_bytes_per_launch": alg,
-                "note": "algorithmic bytes = input + compressed output per launch (1 + r per input byte); "
-                        "the path is compare/serial-bound, HBM fraction is small by construction",
-                "path_achieved": alg / (main_res["ms_per_step"] * 1e-3) / 1e9}
+                "note": "achieved = (rank-0 shard input + its compressed segment) / k_match's average hipEvent "
+                        "time over the K compress-only steps; traffic = FETCH_SIZE x 2 + WRITE_SIZE per launch "
+                        "from profiles/pmc_latest.json (rocprofv3 PMC passes), scaled to this shard",
+                "path_achieved": alg / (main_res["compress_only"]["ms_per_step"] * 1e-3) / 1e9}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.kind, seeds[args.kind], args.block)
+            cpu = cpu_baseline(args.kind, SEEDS[args.kind], args.block)
+        shard_note = "the whole input" if world == 1 else f"1/{world} of it per rank (contiguous block ranges)"
         line = {
             "metric": METRIC, "value": main_res["value"], "unit": "MB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": main_res["ms_per_step"],
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: glibc rand()%256 seed 4, rank r = bytes [r*shard, (r+1)*shard) of one stream "
-                    "(SURVEY.md §8(d)); extra legs: text = enwik-style generator seed 3+rank at 1 MiB (HL-text) "
-                    "and 256 KiB blocks (c3), zeros, runs seed 5+rank (BASELINE config 5)",
-            "config": {"workload": f"{args.kind} {args.mib} MiB per GPU, {args.block // 1024} KiB blocks "
-                                   f"(BASELINE config 4 sharding; N=1 = HL-{args.kind})",
-                       "kind": args.kind, "bytes_per_gpu": n, "block_bytes": args.block,
-                       "global_bytes": n * world, "parallelism": f"block-sharded x{world}"},
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: glibc rand()%256 seed 4 (SURVEY.md §8(d)); the 1 GiB input is SURVEY's HL-rand "
+                    "(= the first GiB of BASELINE config 4); extra legs: text = enwik-style generator seed 3 at "
+                    "1 MiB (HL-text) and 256 KiB blocks (C3), zeros and runs seed 5 (config 5), dna = "
+                    "'ACGT'[rand()%4] seed 6 (lazy-path stress)",
+            "config": {"workload": f"{args.kind} {main_res['global_bytes'] >> 20} MiB, {args.block // 1024} KiB "
+                                   f"blocks, {shard_note}; step = compress + concatenation of the segments "
+                                   f"into one stream ({main_res['concat']})",
+                       "kind": args.kind, "global_bytes": main_res["global_bytes"],
+                       "bytes_per_gpu": n, "block_bytes": args.block,
+                       "parallelism": f"block-sharded x{world}, RCCL {main_res['concat']}" if world > 1
+                       else "single GPU"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "ratio": main_res["ratio"],
             "bit_exact_vs_reference": main_res.get("bit_exact_vs_reference"),
+            "compress_only": main_res["compress_only"],
+            "concat_ms_per_step": main_res.get("concat_ms_per_step"),
             "stages_ms": main_res["stages_ms"],
             "lazy_evals": main_res["lazy_evals"],
-            "concat": concat,
             "decode": main_res.get("decode"),
             "host_path": main_res.get("host_path"),
         }
         if world == 1 and not args.no_lz78 and not args.no_text:
             line["lz78"] = lz78_leg(dev)
+        keep = ["value", "ms_per_step", "compress_only", "concat_ms_per_step", "ratio", "block_bytes", "stages_ms",
+                "lazy_evals", "lazy_tiles", "decode", "bit_exact_vs_reference"]
         for name, lr in legs.items():
-            line[name] = {k: lr[k] for k in ["value", "ms_per_step", "ratio", "block_bytes", "stages_ms", "lazy_evals"]}
-            if "decode" in lr:
-                line[name]["decode"] = lr["decode"]
-            line[name]["bit_exact_vs_reference"] = lr.get("bit_exact_vs_reference")
+            line[name] = {k: lr[k] for k in keep if k in lr}
+        if weak is not None:
+            line["weak"] = {k: weak[k] for k in keep + ["rank_segments_bit_exact", "global_bytes"] if k in weak}
+            line["weak"]["workload"] = (f"BASELINE config 4 sharding: rank r = bytes [r GiB, (r+1) GiB) of the "
+                                        f"seed-4 rand stream, {world} GiB total, segments gathered to rank 0")
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -121,8 +121,9 @@ int fcx_compress_stream(fcx_ctx *ctx, fcx_read_fn read, fcx_write_fn write, void
 /* Enables per-kernel hipEvent timing of subsequent fcx_compress_shard calls. */
 int fcx_ctx_set_profiling(fcx_ctx *ctx, int enable);
 /* Testing: forces how the match kernel evaluates every tile of later calls —
- * 0 auto (default), 1 bucket search (hash buckets, unknown positions via the run
- * table / the stitch), 2 run table for whole tiles.  The output is identical in
+ * 0 auto (default: run table for tiles of long runs, sparse search where few keys
+ * repeat, else bucket search), 1 bucket search for every tile (unknown positions
+ * via the run table / the stitch), 2 run table for whole tiles.  The output is identical in
  * every mode; only the speed differs. */
 int fcx_ctx_set_match_mode(fcx_ctx *ctx, int mode);
 /* After a profiled call: number of stages, and stage i's name and device ms. */

@@ -250,7 +250,7 @@ int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
 int fcx_ctx_set_match_mode(fcx_ctx *c, int mode) {
     if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
     if (mode < 0 || mode > 2) return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search) or 2 (run table)");
-    c->match_mode = mode == 1 ? 4u : mode == 2 ? 8u : 0u;   // k_match dbg bits 2 / 3: both keep the output exact
+    c->match_mode = mode == 1 ? 4u | 128u : mode == 2 ? 8u : 0u;   // k_match dbg bits: all keep the output exact
     return FCX_OK;
 }
 

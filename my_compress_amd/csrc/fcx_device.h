@@ -20,7 +20,8 @@ constexpr uint32_t kHashBits = 13;
 constexpr uint32_t kHalo = kWin;                     // left halo of a tile
 constexpr uint32_t kLookAhead = 260;                 // right look-ahead bytes (>= 257)
 constexpr uint32_t kTileBytes = 6464;                // >= kHalo + kTile + kLookAhead, x64
-constexpr uint32_t kMaxChainSteps = 96;              // per-position candidate budget before "unknown"
+constexpr uint32_t kMaxChainSteps = 1024;            // per-position candidate budget before "unknown"
+constexpr uint32_t kExtBudget = 24;                  // per-position long-match extensions before "unknown"
 constexpr uint32_t kDenseUnknowns = 512;             // tile gives up all-position search past this
 constexpr uint32_t kChunk = 8192;                    // symbols per histogram / encode workgroup
 constexpr uint32_t kStreams = 4;                     // flags, chars, p-bits, golomb words

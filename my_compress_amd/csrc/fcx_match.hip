@@ -20,9 +20,12 @@
 //      the mbits bitmap by one ballot per wave: random data writes almost no m).  A
 //      candidate's key check and length come from three dword compares against
 //      the query's preloaded bytes 0..11; only a match reaching 12 bytes enters
-//      the extension loop.  A bucket with more than kMaxChainSteps entries makes the position
-//      "unknown" at once, for the stitch kernel's wave-parallel evaluation
-//      (runs / zeros: long matches, few tokens);
+//      the extension loop.  A candidate right of the current best is skipped when
+//      it cannot be longer (best at the cap, or its byte at the best length
+//      differs).  A bucket with more than kMaxChainSteps entries, or a query with
+//      more than kExtBudget long extensions (periodic data), leaves the position
+//      "unknown" for the run table / the stitch kernel's wave-parallel evaluation
+//      (runs / zeros / short periods: long matches, few tokens);
 //   4. greedy parse of the tile assuming a token starts at t0: each lane walks
 //      its 8 positions, lanes agree on sub-segment entries by a Jacobi fixed
 //      point (entry_{k+1} = exit of sub-segment k walked from entry_k) that
@@ -43,8 +46,20 @@ constexpr uint32_t kIlp = 4;                         // interleaved chain walks 
 constexpr uint32_t kWaves = kMT / 64;
 constexpr uint32_t kHeadWords = (1u << kHashBits) / 2 + 4;                 // u16 counters + sentinel
 constexpr uint32_t kEntWords = kWinPos / 2;                                 // u16 entries
-constexpr uint32_t kRegionWords = kHeadWords + kEntWords > kTile / 2 + 3 * kMT + 1
+constexpr uint32_t kIns = kWinPos / kMT;              // 12 window positions per lane (insert / filter)
+static_assert(kIns * kMT == kWinPos && kIns == 12, "12 consecutive window positions per lane");
+// repeat filter: "seen" and "dup" bitmaps of 17-bit key hashes (2 x 16 KiB)
+constexpr uint32_t kFilterBits = 17;
+constexpr uint32_t kFilterWords = 2 * (1u << kFilterBits) / 32;
+constexpr uint32_t kSparseEvents = 512;              // repeats up to which the sparse search runs
+constexpr uint32_t kSparseBuckets = 1024;            // buckets of the sparse search's counting sort
+// sparse-search layout inside the region (words): step (u16 x 4096) | P | counters | sorted | mbits
+constexpr uint32_t kSpP = kTile / 2, kSpCnt = kSpP + 2 * kSparseEvents, kSpSrt = kSpCnt + kSparseBuckets / 2 + 16,
+                   kSpMb = kSpSrt + kSparseEvents + 64;
+static_assert(kSpMb + 128 <= kFilterWords, "sparse layout");
+constexpr uint32_t kBucketWords = kHeadWords + kEntWords > kTile / 2 + 3 * kMT + 1
                                       ? kHeadWords + kEntWords : kTile / 2 + 3 * kMT + 1;
+constexpr uint32_t kRegionWords = kBucketWords > kFilterWords ? kBucketWords : kFilterWords;
 // dense-window phase (run table) inside the same region
 constexpr uint32_t kRunBmWords = 208;                // 6656 bitmap positions >= kTileBytes + 1, 13 x kMT
 constexpr uint32_t kRunListWords = 2 * 64 * kWaves;   // per-wave candidate lists (se, ext)
@@ -54,6 +69,11 @@ static_assert(kRunBmWords <= 4 * 64, "prefix scan spans four waves");
 static_assert(kRunTableCap >= 1536, "run table");
 
 __device__ inline uint32_t key_mix(uint32_t key) { return (key * 0x9E3779B1u) & 0xFFFFFFu; }  // bijective mod 2^24
+
+// lanes below this one with their bit set in a wave mask
+__device__ inline uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 // ---- 3b. dense windows (zeros, runs): the positions the bucket search left
 // "unknown" get their exact match from the run table (run_match, fcx_device.h).
@@ -192,6 +212,134 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
     __syncthreads();
 }
 
+// ---- 2b. sparse search (few repeated keys: random data).  P = the window positions whose
+// 17-bit hash repeats (<= 2 x repeats), counting-sorted by 10 hash bits; each P position
+// inside the tile scans its bucket exactly like the bucket search (key check by dword
+// compare, leftmost maximum, extension budget); every other position is a literal.
+// Writes step (LDS), m and the tile's mbits words.  Kept out of line: its registers do
+// not weigh on the bucket search.
+__device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region, uint32_t kw0, uint32_t kw1,
+                                           uint32_t kw2, uint32_t kw3, uint32_t *s_red,
+                                           uint32_t *s_np, uint32_t *s_unknown, uint32_t *s_match, uint32_t *mrow,
+                                           uint64_t *mbw, uint32_t q0, uint32_t npos, uint32_t ins_end, uint32_t w0,
+                                           uint32_t blen, uint32_t ntile, uint32_t dbg) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t kw[4] = {kw0, kw1, kw2, kw3};
+    auto hash_of = [&](uint32_t r) -> uint32_t {
+        return key_mix(__builtin_amdgcn_alignbyte(kw[(r >> 2) + 1], kw[r >> 2], r & 3) & 0xFFFFFFu);
+    };
+    const uint32_t *dupm = region + kFilterWords / 2;
+    uint16_t *step = (uint16_t *)region;
+    {
+        uint32_t *P = region + kSpP;
+        uint32_t *cnt = region + kSpCnt;
+        const uint16_t *c16 = (const uint16_t *)cnt;
+        uint16_t *srt = (uint16_t *)(region + kSpSrt);
+        uint64_t *mbl = (uint64_t *)(region + kSpMb);
+        for (uint32_t x = tid; x < kTile / 2; x += kMT) region[x] = 0x00010001u;   // step = 1 (literal)
+        for (uint32_t x = tid; x <= kSparseBuckets / 2; x += kMT) cnt[x] = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < kIns; r++) {
+            const uint32_t x = kIns * tid + r;
+            const uint32_t hf = hash_of(r) >> (24 - kFilterBits);
+            const bool f = x < ins_end && ((dupm[hf >> 5] >> (hf & 31)) & 1u);
+            const uint64_t bal = __ballot(f);
+            if (bal) {
+                uint32_t base = 0;
+                if ((tid & 63) == 0) base = atomicAdd(s_np, (uint32_t)__popcll(bal));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (f) P[base + lanes_below(bal)] = x | (hf << 13);
+            }
+        }
+        __syncthreads();
+        const uint32_t np = *s_np;
+        uint32_t pe[2], prk[2];
+#pragma unroll
+        for (uint32_t r = 0; r < 2; r++) {
+            const uint32_t idx = tid + kMT * r;
+            pe[r] = 0xFFFFFFFFu;
+            prk[r] = 0;
+            if (idx < np) {
+                pe[r] = P[idx];
+                const uint32_t bk = (pe[r] >> 13) & (kSparseBuckets - 1), sh = 16 * (bk & 1);
+                prk[r] = (atomicAdd(&cnt[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
+            }
+        }
+        __syncthreads();
+        {   // exclusive scan of the counters, one dword (two buckets) per lane
+            static_assert(kSparseBuckets / 2 == kMT, "one counter dword per lane");
+            const uint32_t c = cnt[tid], sum = (c & 0xFFFFu) + (c >> 16);
+            const uint32_t inc = wave_incl_scan(sum);
+            if ((tid & 63) == 63) s_red[tid >> 6] = inc;
+            __syncthreads();
+            uint32_t pre = inc - sum;
+            for (uint32_t w = 0; w < (tid >> 6); w++) pre += s_red[w];
+            cnt[tid] = pre | ((pre + (c & 0xFFFFu)) << 16);
+            if (tid == 0) cnt[kSparseBuckets / 2] = np;   // start[kSparseBuckets]
+        }
+        if (tid < 64) mbl[tid] = 0;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t r = 0; r < 2; r++)
+            if (pe[r] != 0xFFFFFFFFu) srt[c16[(pe[r] >> 13) & (kSparseBuckets - 1)] + prk[r]] = (uint16_t)(pe[r] & 0x1FFFu);
+        __syncthreads();
+        if (dbg & 32u) return;   // timing: + filter and sparse sort
+#pragma unroll
+        for (uint32_t r = 0; r < 2; r++) {
+            if (pe[r] == 0xFFFFFFFFu) continue;
+            const uint32_t x = pe[r] & 0x1FFFu;
+            const uint32_t i = w0 + x;
+            if (x < q0 || x >= npos || i == 0 || blen - i < 4 || (dbg & 1u)) continue;
+            const uint32_t cap = min(kMaxL, blen - i) - 1;
+            const uint32_t qa = lds_ld4(sdw, x), qb = lds_ld4(sdw, x + 4), qc = lds_ld4(sdw, x + 8);
+            const uint32_t bk = (pe[r] >> 13) & (kSparseBuckets - 1);
+            const uint32_t xlo = max(i, kWin) - kWin - w0;
+            uint32_t best = 0, next = 0;
+            bool unk = false;
+            for (uint32_t e = c16[bk], e1 = c16[bk + 1]; e < e1; e++) {
+                const uint32_t xe = srt[e];
+                if (xe >= x || xe < xlo) continue;
+                const uint32_t wb = xe >> 2, sb = xe & 3;
+                const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1], w_2 = sdw[wb + 2], w_3 = sdw[wb + 3];
+                const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa;
+                if (d0 & 0xFFFFFFu) continue;   // other key
+                uint32_t Lc;
+                if (d0) Lc = 3;
+                else {
+                    const uint32_t d1 = __builtin_amdgcn_alignbyte(w_2, w_1, sb) ^ qb;
+                    if (d1) Lc = 4 + (__builtin_ctz(d1) >> 3);
+                    else {
+                        const uint32_t d2 = __builtin_amdgcn_alignbyte(w_3, w_2, sb) ^ qc;
+                        if (d2) Lc = 8 + (__builtin_ctz(d2) >> 3);
+                        else {
+                            const uint32_t bL = best >> 13, bxe = 8191u - (best & 0x1FFFu);
+                            if (cap <= 12 || (dbg & 2u) ||
+                                (bL >= 12 && xe > bxe && (bL >= cap || lds_ld1(sdw, xe + bL) != lds_ld1(sdw, x + bL))))
+                                Lc = 12;
+                            else {
+                                if (++next > kExtBudget) { unk = true; break; }
+                                Lc = lds_match_len(sdw, xe, x, 12, cap);
+                            }
+                        }
+                    }
+                }
+                Lc = min(Lc, cap);
+                best = max(best, (Lc << 13) | (8191u - xe));
+            }
+            const uint32_t Lb = best >> 13;
+            if (unk || Lb >= kMinL) {
+                mrow[x] = unk ? kUnknown : m_pack(Lb, x - (8191u - (best & 0x1FFFu)));
+                step[x - q0] = (uint16_t)(unk ? 0u : Lb + 1);
+                atomicOr(&mbl[(x - q0) >> 6], 1ull << ((x - q0) & 63));
+                if (unk) *s_unknown = 1;
+                else *s_match = 1;
+            }
+        }
+        __syncthreads();
+        if (tid < (ntile + 63) / 64) mbw[tid] = mbl[tid];
+    }
+}
+
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
@@ -206,6 +354,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
     __shared__ uint32_t s_nruns;
+    __shared__ uint32_t s_events;   // repeat filter: window keys whose hash was seen before
+    __shared__ uint32_t s_np;       // sparse search: positions whose hash repeats
     __shared__ uint32_t s_chg[2];
     __shared__ uint32_t s_red[3 * kWaves];   // cross-wave scan partials
 
@@ -278,25 +428,70 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     const bool rmode = (s_nruns <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
     if (dbg & 16u) return;   // timing: staging + run count only
 
+    // this lane's 12 consecutive window positions 12 tid .. 12 tid + 11 take their keys from
+    // bytes [12 tid, 12 tid + 16) of the image, held in registers (stride-3 dword reads:
+    // conflict-free)
+    const uint32_t ins_end = min(npos, blen >= 3 ? blen - 2 - w0 : 0);  // j + 3 <= blen
+    uint32_t kw[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) kw[q] = sdw[kIns / 4 * tid + q];
+    auto hash_of = [&](uint32_t r) -> uint32_t {   // r: compile-time after unrolling
+        return key_mix(__builtin_amdgcn_alignbyte(kw[(r >> 2) + 1], kw[r >> 2], r & 3) & 0xFFFFFFu);
+    };
+
     if (rmode) {
         for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
         if (tid == 0) s_unknown = 1;
         __syncthreads();
+    } else {
+    // ---- 2a. repeat filter: every window key's 17-bit hash goes into "seen"; a hash
+    // seen before goes into "dup" and counts as a repeat.  Random data has a few
+    // hundred repeats per tile (almost all hash collisions), so the search below
+    // visits only the positions whose hash repeats (sparse search); above
+    // kSparseEvents repeats the tile takes the bucket search. ----
+    uint32_t *seen = region, *dupm = region + kFilterWords / 2;
+    {
+        uint4 *r4 = (uint4 *)region;
+        for (uint32_t x = tid; x < kFilterWords / 4; x += kMT) r4[x] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid == 0) { s_events = 0; s_np = 0; }
+    __syncthreads();
+    {
+        uint32_t ev = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < kIns; r++) {
+            if (kIns * tid + r < ins_end) {
+                const uint32_t hf = hash_of(r) >> (24 - kFilterBits);
+                const uint32_t bit = 1u << (hf & 31);
+                if (atomicOr(&seen[hf >> 5], bit) & bit) {
+                    atomicOr(&dupm[hf >> 5], bit);
+                    ev++;
+                }
+            }
+        }
+        ev = wave_sum_u32(ev);
+        if ((tid & 63) == 0 && ev) atomicAdd(&s_events, ev);
+    }
+    __syncthreads();
+    const bool sparse = s_events <= kSparseEvents && !(dbg & 128u);
+
+    if (sparse) {
+        sparse_search(sdw, region, kw[0], kw[1], kw[2], kw[3], s_red, &s_np, &s_unknown, &s_match, m + bstart + w0,
+                      mbits + (uint64_t)b * L.wpb + (t0 >> 6), q0, npos, ins_end, w0, blen, t1 - t0, dbg);
+        __syncthreads();
+        if (dbg & 32u) return;
     } else {
     for (uint32_t x = tid; x < kHeadWords; x += kMT) hw[x] = 0;
     __syncthreads();
 
     // ---- 2. counting sort of the window positions by bucket ----
     // 16-bit counters, two per dword (a bucket never exceeds 6144 entries)
-    const uint32_t ins_end = min(npos, blen >= 3 ? blen - 2 - w0 : 0);  // j + 3 <= blen
-    constexpr uint32_t kIns = (kWinPos + kMT - 1) / kMT;               // 12 per lane
     uint32_t ins_hr[kIns];                                             // bucket << 16 | tag << 13 | rank
 #pragma unroll
     for (uint32_t r = 0; r < kIns; r++) {
-        const uint32_t x = tid + kMT * r;
         ins_hr[r] = 0xFFFFFFFFu;
-        if (x < ins_end) {
-            const uint32_t h = key_mix(lds_key3(sdw, x));
+        if (kIns * tid + r < ins_end) {
+            const uint32_t h = hash_of(r);
             const uint32_t bk = h >> (24 - kHashBits), sh = 16 * (bk & 1);
             const uint32_t old = atomicAdd(&hw[bk >> 1], 1u << sh);
             ins_hr[r] = (bk << 16) | ((h & 7u) << 13) | ((old >> sh) & 0x1FFFu);   // rank < 6144
@@ -327,9 +522,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 #pragma unroll
     for (uint32_t r = 0; r < kIns; r++)
         if (ins_hr[r] != 0xFFFFFFFFu) {
-            const uint32_t x = tid + kMT * r;
             const uint32_t bk = ins_hr[r] >> 16;
-            ent[h16[bk] + (ins_hr[r] & 0x1FFFu)] = (uint16_t)((ins_hr[r] & 0xE000u) | x);
+            ent[h16[bk] + (ins_hr[r] & 0x1FFFu)] = (uint16_t)((ins_hr[r] & 0xE000u) | (kIns * tid + r));
         }
     __syncthreads();
 
@@ -358,7 +552,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     const uint32_t h = key_mix(qa[u] & 0xFFFFFFu);
                     const uint32_t bk = h >> (24 - kHashBits);
                     const uint32_t lo = h16[bk], n = h16[bk + 1] - lo;
-                    xpk[u] = x | (cap << 13) | ((h & 7u) << 22);
+                    xpk[u] = x | (cap << 13) | ((h & 7u) << 22);   // bits 25..31: extension count
                     if (n > kMaxChainSteps) rng[u] = 0xFFFFFFFFu;
                     else { rng[u] = lo | (n << 16); nmax = max(nmax, n); }
                 }
@@ -372,13 +566,13 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                 const uint32_t xe = nd & 0x1FFFu;
                 const uint32_t x = xpk[u] & 0x1FFFu;
                 const uint32_t xlo = max(w0 + x, kWin) - kWin - w0;
-                if ((nd >> 13) != (xpk[u] >> 22) || xe >= x || xe < xlo) continue;
+                if (((nd >> 13) & 7u) != ((xpk[u] >> 22) & 7u) || xe >= x || xe < xlo) continue;
+                const uint32_t cap = (xpk[u] >> 13) & 0x1FFu;
                 // bytes 0..11 of the candidate, from four aligned dwords
                 const uint32_t wb = xe >> 2, sb = xe & 3;
                 const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1], w_2 = sdw[wb + 2], w_3 = sdw[wb + 3];
                 const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa[u];
                 if (d0 & 0xFFFFFFu) continue;   // 3-tag-bit collision: different key
-                const uint32_t cap = (xpk[u] >> 13) & 0x1FFu;
                 uint32_t Lc;
                 if (d0) Lc = 3;
                 else {
@@ -387,7 +581,22 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     else {
                         const uint32_t d2 = __builtin_amdgcn_alignbyte(w_3, w_2, sb) ^ qc[u];
                         if (d2) Lc = 8 + (__builtin_ctz(d2) >> 3);
-                        else Lc = (cap > 12 && !(dbg & 2u)) ? lds_match_len(sdw, xe, x, 12, cap) : 12;
+                        else {
+                            // >= 12 bytes.  A candidate right of the best (>= 12) wins only if
+                            // longer: not past the cap, not if its byte at the best length differs
+                            const uint32_t bL = best[u] >> 13, bxe = 8191u - (best[u] & 0x1FFFu);
+                            if (cap <= 12 || (dbg & 2u) ||
+                                (bL >= 12 && xe > bxe && (bL >= cap || lds_ld1(sdw, xe + bL) != lds_ld1(sdw, x + bL))))
+                                Lc = 12;
+                            else {
+                                // extension budget per query (periodic data: every same-phase
+                                // candidate runs to the cap); past it the position is left to
+                                // the exact lazy evaluation
+                                xpk[u] += 1u << 25;
+                                if ((xpk[u] >> 25) > kExtBudget) { rng[u] = 0xFFFFFFFFu; continue; }
+                                Lc = lds_match_len(sdw, xe, x, 12, cap);
+                            }
+                        }
                     }
                 }
                 Lc = min(Lc, cap);
@@ -419,6 +628,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     for (uint32_t r = 0; r < kQPL; r++) step[tid + kMT * r] = (uint16_t)(st_reg[r >> 1] >> (16 * (r & 1)));
     __syncthreads();
     }   // bucket search
+    }   // filter: sparse or bucket search
 
     // ---- 3b. dense windows: exact matches of the unknown positions over the run table ----
     const bool dense = s_unknown != 0;   // matches may come from the run table: no fast path below

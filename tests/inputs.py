@@ -9,7 +9,7 @@ import ctypes
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GEN_KIND = {"rand": 0, "zeros": 1, "runs": 2, "text": 3}
+GEN_KIND = {"rand": 0, "zeros": 1, "runs": 2, "text": 3, "dna": 4}
 MiB = 1 << 20
 
 _gen = None
@@ -184,12 +184,13 @@ C4_SEGMENTS = [
 C4_FILE = {"bytes": 8730352595, "out": "8f1cae2fa6fbc3b597bd90b83fd0998ffeb7d827e199a9f6aa3c25fea587656c"}
 
 
-def rand_stream_into(seed: int, offset: int, ptr: int, n: int) -> None:
-    """bytes [offset, offset + n) of the rand stream of `seed` (glibc rand()%256),
-    via the generator's O(log offset) jump-ahead: rank shards of one global input"""
+def rand_stream_into(seed: int, offset: int, ptr: int, n: int, kind: str = "rand") -> None:
+    """bytes [offset, offset + n) of the rand (or dna) stream of `seed` (one glibc
+    rand() per byte), via the generator's O(log offset) jump-ahead: rank shards of
+    one global input"""
     G = gen_lib()
     G.fcxgen_skip.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    h = G.fcxgen_create(GEN_KIND["rand"], seed)
+    h = G.fcxgen_create(GEN_KIND[kind], seed)
     try:
         G.fcxgen_skip(h, offset)
         G.fcxgen_fill(h, ctypes.c_void_p(ptr), n)

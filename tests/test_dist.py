@@ -35,9 +35,21 @@ def _worker(rank, world, port, cases, results):
             for codec, enc in (("lz77", oracle.compress_file), ("lz78", oracle.lz78_compress_file)):
                 seg = enc(data[lo:hi], block)[10:] if hi > lo else b""
                 t = torch.frombuffer(bytearray(seg), dtype=torch.uint8) if seg else torch.zeros(0, dtype=torch.uint8)
-                whole = fdist.concat_segments(t, dist)
+                for mode in ("allgather", "gather"):
+                    whole = fdist.concat_segments(t, dist, mode=mode, dst=world - 1 if mode == "gather" else 0)
+                    if whole is not None:
+                        results[(idx, codec, mode, rank)] = fdist.assemble_file(len(data), block,
+                                                                               whole.numpy().tobytes(), codec)
+                # gather into the rank's own output buffer: rank 0's segment already sits at offset 0
+                sizes, offs = fdist.exchange_sizes(t.numel(), dist, t.device)
+                buf = torch.zeros(sum(sizes) + 16, dtype=torch.uint8)
+                if rank == 0 and t.numel():
+                    buf[:t.numel()] = t
+                    t = buf[:t.numel()]
+                n = fdist.gather_segments(t, buf, sizes, offs, dist, 0)
                 if rank == 0:
-                    results[(idx, codec)] = fdist.assemble_file(len(data), block, whole.numpy().tobytes(), codec)
+                    results[(idx, codec, "inplace", 0)] = fdist.assemble_file(len(data), block,
+                                                                             buf[:n].numpy().tobytes(), codec)
     finally:
         dist.destroy_process_group()
 
@@ -54,8 +66,12 @@ def test_two_rank_concat_matches_single_process():
     mp.spawn(_worker, args=(2, _free_port(), cases, results), nprocs=2, join=True)
     for idx, (spec, block) in enumerate(cases):
         data = inputs.make(spec)
-        assert results[(idx, "lz77")] == oracle.compress_file(data, block), idx
-        assert results[(idx, "lz78")] == oracle.lz78_compress_file(data, block), idx
+        want = {"lz77": oracle.compress_file(data, block), "lz78": oracle.lz78_compress_file(data, block)}
+        for codec in ("lz77", "lz78"):
+            for key in [(idx, codec, "allgather", 0), (idx, codec, "allgather", 1), (idx, codec, "gather", 1),
+                        (idx, codec, "inplace", 0)]:
+                assert results[key] == want[codec], key
+            assert (idx, codec, "gather", 0) not in results   # gather lands on dst only
 
 
 def test_block_ranges_partition():

@@ -121,6 +121,15 @@ def test_dense_and_periodic_edges(gpu_compress):
             assert gpu_compress(data, block) == oracle.compress_file(data, block), (len(data), block)
 
 
+@pytest.mark.parametrize("block", [1 << 20, 65536])
+def test_dna_vs_oracle(gpu_compress, block):
+    """'ACGT'[rand()%4]: 64 distinct 3-byte keys, ~32 same-key candidates per
+    position and matches of a few bytes — the bucket budget overflows and the
+    lazy evaluation path (k_stitch, wave-parallel search) carries the parse"""
+    data = inputs.generate("dna", 6, 4 << 20)
+    assert gpu_compress(data, block) == oracle.compress_file(data, block)
+
+
 def test_round_trip_host_decoder(gpu_compress):
     for kind, seed in [("rand", 3), ("text", 4), ("runs", 5)]:
         data = inputs.generate(kind, seed, 3 << 20)

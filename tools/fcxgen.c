@@ -60,7 +60,7 @@ static inline int32_t grand_next(glibc_rand_t *g) {
 }
 
 /* ---- generator state ------------------------------------------------------ */
-enum { GEN_RAND = 0, GEN_ZEROS = 1, GEN_RUNS = 2, GEN_TEXT = 3 };
+enum { GEN_RAND = 0, GEN_ZEROS = 1, GEN_RUNS = 2, GEN_TEXT = 3, GEN_DNA = 4 };
 
 #define TEXT_V 4096
 typedef struct {
@@ -141,6 +141,9 @@ void fcxgen_fill(void *h, uint8_t *out, uint64_t n) {
     case GEN_ZEROS:
         memset(out, 0, n);
         break;
+    case GEN_DNA:   /* "ACGT"[rand() % 4]: a 4-letter alphabet, 64 distinct 3-byte keys */
+        for (; i < n; i++) out[i] = (uint8_t)"ACGT"[grand_next(&s->g) % 4];
+        break;
     case GEN_RUNS:
         while (i < n) {
             if (s->run_left == 0) {
@@ -185,7 +188,7 @@ static void mat_mul(const mat31 *x, const mat31 *y, mat31 *z) {
 
 int fcxgen_skip(void *h, uint64_t k) {
     fcxgen_t *s = (fcxgen_t *)h;
-    if (!s || s->kind != GEN_RAND) return -1;
+    if (!s || (s->kind != GEN_RAND && s->kind != GEN_DNA)) return -1;
     uint32_t st[31], nst[31];
     for (int i = 0; i < 31; i++) st[i] = (uint32_t)s->g.r[(s->g.k + i) % 34u];
     mat31 base, res, tmp;
