@@ -76,10 +76,10 @@ __device__ inline uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+// sum over the 64 lanes (uniform result); every lane of the wave must be active
+__device__ inline uint32_t wave_incl_scan(uint32_t v);
 __device__ inline uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
 __device__ inline uint64_t wave_sum_u64(uint64_t v) {
@@ -92,14 +92,16 @@ __device__ inline uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 
-// inclusive prefix sum across the 64 lanes
+// inclusive prefix sum across the 64 lanes, on the VALU through DPP lane moves (no LDS
+// traffic): row_shr 1/2/4/8 within each row of 16, then row_bcast 15 / 31 carry the row
+// totals upward.  Every lane of the wave must be active.
 __device__ inline uint32_t wave_incl_scan(uint32_t v) {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= (uint32_t)o) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
     return v;
 }
 

@@ -646,6 +646,18 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         return;
     }
 
+    if (s_match == 0 && !dense) {
+        // no match anywhere (most tiles of random data): every position is a literal
+        // token; the chain words, their prefix counts and the totals follow directly
+        if (tid < nwords) {
+            const uint32_t nb = min(64u, t1 - t0 - 64 * tid);
+            cw[tid] = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+            chain_pfx[(uint64_t)blockIdx.x * (kTile / 64) + tid] = 64ull * tid;   // tokens before; no matches
+        }
+        if (tid == 0) { ti[0] = 0; ti[1] = t1; ti[2] = t1 - t0; ti[3] = 0; ti[4] = 0; }
+        return;
+    }
+
     // ---- 4. tile-local greedy parse ----
     uint32_t *Gs = region + kTile / 2;                 // kMT + 1 entries
     uint32_t *Xs = Gs + kMT + 1;
@@ -655,11 +667,6 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     uint32_t V = 0, X = s;
     uint32_t T = 0;
     uint32_t *Ys = Vs;   // exits of a Jacobi round (Vs is free until the counts below)
-    if (s_match == 0 && !dense) {
-        // no match anywhere (most tiles of random data): every position is a literal token
-        if (s < t1) T = se - s == 32 ? ~0u : ((1u << (se - s)) - 1u);
-        if (tid == 0) Gs[(t1 - t0 + kSeg - 1) / kSeg] = t1;
-    } else {
     if (s < t1) {
         uint32_t t = s;
         while (t < se) { V |= 1u << (t - s); t += step[t - t0]; }
@@ -704,7 +711,6 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         __syncthreads();
         if (!s_chg[r & 1]) break;
     }
-    }   // Jacobi
     // counts of this lane's chain positions, prefix over lanes
     uint32_t cnt[3] = {(uint32_t)__builtin_popcount(T), 0, 0};
     for (uint32_t bits = T; bits; bits &= bits - 1) {

@@ -449,8 +449,41 @@ __device__ inline void flush_words(uint32_t *g, uint32_t gw0, const uint32_t *w,
     }
 }
 
+// all-literal tile (random data): the tile's chars are its input bytes, its flags all
+// ones; copied at the tile's unaligned stream offsets without staging
+__device__ void emit_literal_tile(const uint8_t *d, const uint32_t *d32, uint64_t avail, uint32_t t0, uint32_t nt,
+                                  uint32_t tok0, uint8_t *chars, uint32_t *flags) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t a = (tok0 + 3) & ~3u, z = (tok0 + nt) & ~3u;   // [a, z): whole output dwords
+    const uint32_t sh = (t0 - tok0) & 3u;
+    for (uint32_t q = (a >> 2) + tid; q < (z >> 2); q += 256) {
+        const uint32_t so = t0 + 4 * q - tok0;   // input byte of output byte 4q
+        const uint32_t wi = so >> 2;
+        const uint32_t lo = d32[wi];
+        uint32_t v = lo;
+        if (sh) {
+            uint32_t hi = 0;
+            if (4ull * wi + 8 <= avail) hi = d32[wi + 1];
+            else
+                for (uint32_t j = 0; j < 4 && 4ull * wi + 4 + j < avail; j++) hi |= (uint32_t)d[4 * wi + 4 + j] << (8 * j);
+            v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        }
+        ((uint32_t *)chars)[q] = v;
+    }
+    const uint32_t head_end = min(a, tok0 + nt);
+    if (tid < head_end - tok0) chars[tok0 + tid] = d[t0 + tid];
+    if (z >= a && tid < tok0 + nt - z) chars[z + tid] = d[t0 + z - tok0 + tid];
+    const uint32_t f0 = tok0, f1 = tok0 + nt;
+    for (uint32_t w = (f0 >> 5) + tid; w <= ((f1 - 1) >> 5); w += 256) {
+        const uint32_t lo = max(f0, 32 * w), hi = min(f1, 32 * w + 32);
+        if (hi - lo == 32) flags[w] = ~0u;
+        else atomicOr(&flags[w], ((1u << (hi - lo)) - 1u) << (lo - 32 * w));
+    }
+}
+
 __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
                                               const uint64_t *__restrict__ mbits, const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
+                                              const BlockInfo *__restrict__ binfo,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb) {
     __shared__ uint32_t sh[12];
@@ -462,6 +495,18 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     const uint32_t t0 = k * kTile;
     if (t0 >= blen) return;
     const uint32_t t1 = min(blen, t0 + kTile);
+    {   // this tile's token and match counts: the next tile's offsets, or the block totals
+        const uint32_t tix = blockIdx.x;
+        const bool last = t1 == blen;
+        const uint32_t tk0 = tile_off[3 * tix], mk0 = tile_off[3 * tix + 1];
+        const uint32_t tk1 = last ? binfo[b].ntok : tile_off[3 * tix + 3];
+        const uint32_t mk1 = last ? binfo[b].nmatch : tile_off[3 * tix + 4];
+        if (tk1 - tk0 == t1 - t0 && mk1 == mk0 && ((uintptr_t)(in + bstart) & 3) == 0) {
+            emit_literal_tile(in + bstart, (const uint32_t *)(in + bstart), L.n - bstart, t0, t1 - t0, tk0,
+                              s_chars + (uint64_t)b * L.sstride[1], (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]));
+            return;
+        }
+    }
 
     // this lane's 16 positions: one quarter of a chain word
     const uint32_t s = t0 + tid * 16;
@@ -604,8 +649,8 @@ void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_
     hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, tile_off,
                        binfo);
     if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, s_flags, s_chars,
-                       s_p, s_golomb);
+    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, s_flags,
+                       s_chars, s_p, s_golomb);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 
