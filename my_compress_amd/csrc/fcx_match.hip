@@ -52,6 +52,8 @@ static_assert(kIns * kMT == kWinPos && kIns == 12, "12 consecutive window positi
 constexpr uint32_t kFilterBits = 17;
 constexpr uint32_t kFilterWords = 2 * (1u << kFilterBits) / 32;
 constexpr uint32_t kSparseEvents = 512;              // repeats up to which the sparse search runs
+constexpr uint32_t kSampleWords = 128;               // repeat sample: 2^12-bit bitmap of 512 sampled keys
+constexpr uint32_t kSampleEvents = 96;               // sampled repeats above which the filter is skipped
 constexpr uint32_t kSparseBuckets = 1024;            // buckets of the sparse search's counting sort
 // sparse-search layout inside the region (words): step (u16 x 4096) | P | counters | sorted | mbits
 constexpr uint32_t kSpP = kTile / 2, kSpCnt = kSpP + 2 * kSparseEvents, kSpSrt = kSpCnt + kSparseBuckets / 2 + 16,
@@ -212,6 +214,44 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
     __syncthreads();
 }
 
+// one candidate xe (image position, already known to lie in the window left of x) of
+// query x with preloaded bytes qa/qb/qc: key check and match length from four aligned
+// dwords; >= 12 bytes extend byte-exactly, under a per-query extension budget (periodic
+// data: every same-phase candidate runs to the cap), past which the query is unknown.
+// A candidate right of the best (>= 12) can only win by being longer: skipped at the cap
+// or when its byte at the best length differs.  best = L << 13 | (8191 - position):
+// its maximum is the longest, then leftmost match.
+__device__ inline void scan_candidate(const uint32_t *sdw, uint32_t xe, uint32_t x, uint32_t qa, uint32_t qb,
+                                      uint32_t qc, uint32_t cap, uint32_t &best, uint32_t &next, bool &unk,
+                                      uint32_t dbg) {
+    const uint32_t wb = xe >> 2, sb = xe & 3;
+    const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1], w_2 = sdw[wb + 2], w_3 = sdw[wb + 3];
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa;
+    if (d0 & 0xFFFFFFu) return;   // other key (hash collision)
+    uint32_t Lc;
+    if (d0) Lc = 3;
+    else {
+        const uint32_t d1 = __builtin_amdgcn_alignbyte(w_2, w_1, sb) ^ qb;
+        if (d1) Lc = 4 + (__builtin_ctz(d1) >> 3);
+        else {
+            const uint32_t d2 = __builtin_amdgcn_alignbyte(w_3, w_2, sb) ^ qc;
+            if (d2) Lc = 8 + (__builtin_ctz(d2) >> 3);
+            else {
+                const uint32_t bL = best >> 13, bxe = 8191u - (best & 0x1FFFu);
+                if (cap <= 12 || (dbg & 2u) ||
+                    (bL >= 12 && xe > bxe && (bL >= cap || lds_ld1(sdw, xe + bL) != lds_ld1(sdw, x + bL))))
+                    Lc = 12;
+                else {
+                    if (++next > kExtBudget) { unk = true; return; }
+                    Lc = lds_match_len(sdw, xe, x, 12, cap);
+                }
+            }
+        }
+    }
+    Lc = min(Lc, cap);
+    best = max(best, (Lc << 13) | (8191u - xe));
+}
+
 // ---- 2b. sparse search (few repeated keys: random data).  P = the window positions whose
 // 17-bit hash repeats (<= 2 x repeats), counting-sorted by 10 hash bits; each P position
 // inside the tile scans its bucket exactly like the bucket search (key check by dword
@@ -296,35 +336,9 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
             const uint32_t xlo = max(i, kWin) - kWin - w0;
             uint32_t best = 0, next = 0;
             bool unk = false;
-            for (uint32_t e = c16[bk], e1 = c16[bk + 1]; e < e1; e++) {
+            for (uint32_t e = c16[bk], e1 = c16[bk + 1]; e < e1 && !unk; e++) {
                 const uint32_t xe = srt[e];
-                if (xe >= x || xe < xlo) continue;
-                const uint32_t wb = xe >> 2, sb = xe & 3;
-                const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1], w_2 = sdw[wb + 2], w_3 = sdw[wb + 3];
-                const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa;
-                if (d0 & 0xFFFFFFu) continue;   // other key
-                uint32_t Lc;
-                if (d0) Lc = 3;
-                else {
-                    const uint32_t d1 = __builtin_amdgcn_alignbyte(w_2, w_1, sb) ^ qb;
-                    if (d1) Lc = 4 + (__builtin_ctz(d1) >> 3);
-                    else {
-                        const uint32_t d2 = __builtin_amdgcn_alignbyte(w_3, w_2, sb) ^ qc;
-                        if (d2) Lc = 8 + (__builtin_ctz(d2) >> 3);
-                        else {
-                            const uint32_t bL = best >> 13, bxe = 8191u - (best & 0x1FFFu);
-                            if (cap <= 12 || (dbg & 2u) ||
-                                (bL >= 12 && xe > bxe && (bL >= cap || lds_ld1(sdw, xe + bL) != lds_ld1(sdw, x + bL))))
-                                Lc = 12;
-                            else {
-                                if (++next > kExtBudget) { unk = true; break; }
-                                Lc = lds_match_len(sdw, xe, x, 12, cap);
-                            }
-                        }
-                    }
-                }
-                Lc = min(Lc, cap);
-                best = max(best, (Lc << 13) | (8191u - xe));
+                if (xe < x && xe >= xlo) scan_candidate(sdw, xe, x, qa, qb, qc, cap, best, next, unk, dbg);
             }
             const uint32_t Lb = best >> 13;
             if (unk || Lb >= kMinL) {
@@ -354,6 +368,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
     __shared__ uint32_t s_nruns;
+    __shared__ uint32_t s_sample;   // repeat sample: sampled keys whose hash was seen before
     __shared__ uint32_t s_events;   // repeat filter: window keys whose hash was seen before
     __shared__ uint32_t s_np;       // sparse search: positions whose hash repeats
     __shared__ uint32_t s_chg[2];
@@ -391,7 +406,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             sdw[x] = v;
         }
     }
-    if (tid == 0) { s_unknown = 0; s_match = 0; s_nruns = 0; s_chg[0] = 0; s_chg[1] = 0; }
+    if (tid == 0) { s_unknown = 0; s_match = 0; s_nruns = 0; s_sample = 0; s_chg[0] = 0; s_chg[1] = 0; }
+    if (tid < kSampleWords) region[tid] = 0;
     __syncthreads();
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
@@ -416,6 +432,18 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         uint32_t cnt = (tid == 0 && nload > 0 ? 1u : 0u) + runs_in(tid);
         cnt = wave_sum_u32(cnt);
         if ((tid & 63) == 0) atomicAdd(&s_nruns, cnt);
+        {   // repeat sample: the key of every 12th window position into a 2^12-bit bitmap;
+            // random data repeats ~32 times in 512 samples, text far more often
+            const uint32_t x = kIns * tid;
+            bool rep = false;
+            if (x + 3 <= nload) {
+                const uint32_t hs = key_mix(lds_key3(sdw, x)) >> 12;
+                const uint32_t bit = 1u << (hs & 31);
+                rep = (atomicOr(&region[hs >> 5], bit) & bit) != 0;
+            }
+            const uint64_t bal = __ballot(rep);
+            if ((tid & 63) == 0 && bal) atomicAdd(&s_sample, (uint32_t)__popcll(bal));
+        }
         __syncthreads();
         if (s_nruns <= kRunTile) {
             cnt = 0;
@@ -444,11 +472,13 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if (tid == 0) s_unknown = 1;
         __syncthreads();
     } else {
-    // ---- 2a. repeat filter: every window key's 17-bit hash goes into "seen"; a hash
-    // seen before goes into "dup" and counts as a repeat.  Random data has a few
-    // hundred repeats per tile (almost all hash collisions), so the search below
-    // visits only the positions whose hash repeats (sparse search); above
-    // kSparseEvents repeats the tile takes the bucket search. ----
+    // ---- 2a. repeat filter (tiles whose sample repeats little): every window key's
+    // 17-bit hash goes into "seen"; a hash seen before goes into "dup" and counts as a
+    // repeat.  Random data has a few hundred repeats per tile (almost all hash
+    // collisions), so the search below visits only the positions whose hash repeats
+    // (sparse search); above kSparseEvents repeats the tile takes the bucket search. ----
+    bool sparse = false;
+    if (s_sample <= kSampleEvents && !(dbg & 128u)) {
     uint32_t *seen = region, *dupm = region + kFilterWords / 2;
     {
         uint4 *r4 = (uint4 *)region;
@@ -473,7 +503,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if ((tid & 63) == 0 && ev) atomicAdd(&s_events, ev);
     }
     __syncthreads();
-    const bool sparse = s_events <= kSparseEvents && !(dbg & 128u);
+    sparse = s_events <= kSparseEvents;
+    }   // repeat filter
 
     if (sparse) {
         sparse_search(sdw, region, kw[0], kw[1], kw[2], kw[3], s_red, &s_np, &s_unknown, &s_match, m + bstart + w0,
@@ -490,8 +521,12 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 #pragma unroll
     for (uint32_t r = 0; r < kIns; r++) {
         ins_hr[r] = 0xFFFFFFFFu;
-        if (kIns * tid + r < ins_end) {
-            const uint32_t h = hash_of(r);
+        // position-strided (x = tid + kMT r): ranks within a bucket come out roughly in
+        // position order, so a query meets its leftmost candidates first (fewer long
+        // extensions survive the right-of-best pruning); measured faster than keys from
+        // the lane's registers on text and dna
+        if (tid + kMT * r < ins_end) {
+            const uint32_t h = key_mix(lds_key3(sdw, tid + kMT * r));
             const uint32_t bk = h >> (24 - kHashBits), sh = 16 * (bk & 1);
             const uint32_t old = atomicAdd(&hw[bk >> 1], 1u << sh);
             ins_hr[r] = (bk << 16) | ((h & 7u) << 13) | ((old >> sh) & 0x1FFFu);   // rank < 6144
@@ -523,7 +558,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     for (uint32_t r = 0; r < kIns; r++)
         if (ins_hr[r] != 0xFFFFFFFFu) {
             const uint32_t bk = ins_hr[r] >> 16;
-            ent[h16[bk] + (ins_hr[r] & 0x1FFFu)] = (uint16_t)((ins_hr[r] & 0xE000u) | (kIns * tid + r));
+            ent[h16[bk] + (ins_hr[r] & 0x1FFFu)] = (uint16_t)((ins_hr[r] & 0xE000u) | (tid + kMT * r));
         }
     __syncthreads();
 
