@@ -14,10 +14,10 @@
 
 namespace fcx {
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                  uint64_t *chain_pfx, uint32_t *tinfo, hipStream_t st, uint32_t dbg_override = ~0u);
+                  uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
-                  const uint64_t *chain_pfx,
-                  const uint32_t *tinfo, uint64_t *fp, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
+                  const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
+                  uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
                   uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev);
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
                     uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_bits,
@@ -89,6 +89,8 @@ struct fcx_ctx {
     uint64_t *chain_pfx = nullptr;     // per 64 positions: speculative prefix counts (k_match)
     uint32_t *tinfo = nullptr;         // per tile: flags, exit, token/match/golomb-bit totals
     uint32_t *tile_off = nullptr;      // per tile: token/match/golomb-bit offsets (k_stitch)
+    uint32_t *mtok = nullptr;          // per tile: compact match list of the speculative chain (k_match)
+    uint32_t *tconv = nullptr;         // per tile: where the final chain joins it (k_resolve / k_stitch)
     uint64_t *fp = nullptr;            // per tile: fast-path record (k_resolve)
     BlockInfo *binfo = nullptr;
     uint8_t *s[kStreams] = {nullptr, nullptr, nullptr, nullptr};
@@ -110,12 +112,13 @@ struct fcx_ctx {
 
 namespace {
 void free_scratch(fcx_ctx *c) {
-    void *ptrs[] = {c->m,    c->mbits, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->fp, c->binfo,
+    void *ptrs[] = {c->m,    c->mbits, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->mtok, c->tconv, c->fp, c->binfo,
                     c->s[0], c->s[1],  c->s[2],      c->s[3],       c->hist,     c->ctab,     c->chunk_bits,
                     c->ltab, c->hhdr,  c->blk_off};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     c->m = nullptr; c->mbits = c->chain = c->chain_pfx = c->fp = nullptr; c->tinfo = c->tile_off = nullptr;
+    c->mtok = c->tconv = nullptr;
     c->binfo = nullptr;
     for (auto &p : c->s) p = nullptr;
     c->hist = c->ctab = c->chunk_bits = nullptr;
@@ -144,6 +147,8 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     if ((r = dalloc(&c->chain_pfx, 8ull * (kTile / 64) * nt, "chain_pfx"))) return r;
     if ((r = dalloc(&c->tinfo, 32 * nt, "tinfo"))) return r;
     if ((r = dalloc(&c->tile_off, 12 * nt, "tile_off"))) return r;
+    if ((r = dalloc(&c->mtok, 4ull * kTileMatches * nt, "mtok"))) return r;
+    if ((r = dalloc(&c->tconv, 4 * nt, "tconv"))) return r;
     if ((r = dalloc(&c->fp, 64 * nt, "fp"))) return r;
     if ((r = dalloc(&c->binfo, sizeof(BlockInfo) * nb, "binfo"))) return r;
     for (uint32_t s = 0; s < kStreams; s++)
@@ -297,10 +302,10 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     HIP_TRY(hipMemsetAsync(c->s[2], 0, (uint64_t)L.sstride[2] * L.nblocks, st));
     HIP_TRY(hipMemsetAsync(c->s[3], 0, (uint64_t)L.sstride[3] * L.nblocks, st));
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
-    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, st, c->match_mode);
+    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok, st, c->match_mode);
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
-    launch_parse(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->fp, c->tile_off, c->binfo, c->s[0], c->s[1], c->s[2],
-                 c->s[3], st, ev ? ev + 3 : nullptr);
+    launch_parse(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok, c->fp, c->tile_off, c->tconv,
+                 c->binfo, c->s[0], c->s[1], c->s[2], c->s[3], st, ev ? ev + 3 : nullptr);
     launch_entropy(L, c->binfo, c->s[0], c->s[1], c->s[2], c->s[3], c->hist, c->ctab, c->ltab, c->hhdr,
                    c->chunk_bits, c->blk_off, total, d_out, cap, err, st, ev ? ev + 5 : nullptr);
     HIP_TRY(hipGetLastError());
@@ -345,7 +350,7 @@ int fcx_debug_match(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint32_t dbg, v
     int r = ensure_scratch(c, n);
     if (r) return r;
     const Layout L = make_layout(n, c->B);
-    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, (hipStream_t)stream, dbg);
+    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok, (hipStream_t)stream, dbg);
     HIP_TRY(hipGetLastError());
     return FCX_OK;
 }

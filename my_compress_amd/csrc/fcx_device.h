@@ -35,6 +35,10 @@ __host__ __device__ inline uint32_t m_len(uint32_t m) { return m >> 11; }
 __host__ __device__ inline uint32_t m_dist(uint32_t m) { return m & 0x7FFu; }
 
 constexpr uint32_t kTileLazy = 1u;   // tile_flags: spec parse unavailable, stitch walks it
+constexpr uint32_t kTileMFull = 2u;  // tile_flags: m[] holds every match / unknown of the tile (run table ran)
+constexpr uint32_t kResolveSpan = 256;           // k_resolve's walk limit; m[] rows always kept below it
+constexpr uint32_t kTileMatches = kTile / 4;     // compact match list slots per tile (a match covers >= 4)
+constexpr uint32_t kConvAll = 0xFFFFu;           // tile conv record: k_emit takes every m from m[]
 
 // per-block results of the parse/emit stage
 struct BlockInfo {

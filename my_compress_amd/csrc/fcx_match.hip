@@ -51,17 +51,20 @@ static_assert(kIns * kMT == kWinPos && kIns == 12, "12 consecutive window positi
 // repeat filter: "seen" and "dup" bitmaps of 17-bit key hashes (2 x 16 KiB)
 constexpr uint32_t kFilterBits = 17;
 constexpr uint32_t kFilterWords = 2 * (1u << kFilterBits) / 32;
-constexpr uint32_t kSparseEvents = 512;              // repeats up to which the sparse search runs
+constexpr uint32_t kSparseEvents = 448;              // repeats up to which the sparse search runs
 constexpr uint32_t kSampleWords = 128;               // repeat sample: 2^12-bit bitmap of 512 sampled keys
 constexpr uint32_t kSampleEvents = 96;               // sampled repeats above which the filter is skipped
 constexpr uint32_t kSparseBuckets = 1024;            // buckets of the sparse search's counting sort
 // sparse-search layout inside the region (words): step (u16 x 4096) | P | counters | sorted | mbits
-constexpr uint32_t kSpP = kTile / 2, kSpCnt = kSpP + 2 * kSparseEvents, kSpSrt = kSpCnt + kSparseBuckets / 2 + 16,
-                   kSpMb = kSpSrt + kSparseEvents + 64;
-static_assert(kSpMb + 128 <= kFilterWords, "sparse layout");
+constexpr uint32_t kSpP = kTile / 2, kSpCnt = kSpP + 2 * kSparseEvents, kSpSrt = kSpCnt + kSparseBuckets / 2 + 2,
+                   kSpMb = kSpSrt + kSparseEvents;   // P: u32 x 2 kSparseEvents; srt: u16 x 2 kSparseEvents
+static_assert(kSpMb % 2 == 0 && kSpMb + 128 <= kFilterWords - kTile, "sparse layout below the results");
 constexpr uint32_t kBucketWords = kHeadWords + kEntWords > kTile / 2 + 3 * kMT + 1
                                       ? kHeadWords + kEntWords : kTile / 2 + 3 * kMT + 1;
 constexpr uint32_t kRegionWords = kBucketWords > kFilterWords ? kBucketWords : kFilterWords;
+constexpr uint32_t kResLds = kRegionWords - kTile;   // search results (m) per tile position, kept for the
+                                                     // compact match list; clear of step and the parse scratch
+static_assert(kResLds >= kTile / 2 + 3 * kMT + 1, "results clear of step and the parse scratch");
 // dense-window phase (run table) inside the same region
 constexpr uint32_t kRunBmWords = 208;                // 6656 bitmap positions >= kTileBytes + 1, 13 x kMT
 constexpr uint32_t kRunListWords = 2 * 64 * kWaves;   // per-wave candidate lists (se, ext)
@@ -317,7 +320,7 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
             cnt[tid] = pre | ((pre + (c & 0xFFFFu)) << 16);
             if (tid == 0) cnt[kSparseBuckets / 2] = np;   // start[kSparseBuckets]
         }
-        if (tid < 64) mbl[tid] = 0;
+        if (tid < 64) mbl[tid] = 0;   // (the results array is read only where step marks a match)
         __syncthreads();
 #pragma unroll
         for (uint32_t r = 0; r < 2; r++)
@@ -342,7 +345,9 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
             }
             const uint32_t Lb = best >> 13;
             if (unk || Lb >= kMinL) {
-                mrow[x] = unk ? kUnknown : m_pack(Lb, x - (8191u - (best & 0x1FFFu)));
+                const uint32_t res = unk ? kUnknown : m_pack(Lb, x - (8191u - (best & 0x1FFFu)));
+                mrow[x] = res;
+                region[kResLds + x - q0] = res;
                 step[x - q0] = (uint16_t)(unk ? 0u : Lb + 1);
                 atomicOr(&mbl[(x - q0) >> 6], 1ull << ((x - q0) & 63));
                 if (unk) *s_unknown = 1;
@@ -357,7 +362,7 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
-                                              uint32_t *__restrict__ tinfo, uint32_t dbg) {
+                                              uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg) {
     __shared__ uint32_t sdw[kTileBytes / 4 + 4];           // byte image of the window
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
     // search, [step (u16 x 4096) | parse scratch] after it
@@ -566,9 +571,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // ---- 3. queries: position i = w0 + q0 + tid + kMT*r, kIlp at a time ----
     // per walk: range (start | len << 16), packed best = L << 13 | (8191 - position),
     // query bytes 0..11, x | cap << 13 | tag3 << 22
-    uint32_t st_reg[kQPL / 2];   // step (L+1, 0 = unknown) of query r in half r & 1 of word r >> 1
-#pragma unroll
-    for (uint32_t r = 0; r < kQPL / 2; r++) st_reg[r] = 0x00010001u;
+    uint32_t rs[kQPL];   // result of query r: m (0 = literal, kUnknown)
 #pragma unroll
     for (uint32_t g = 0; g < kQPL; g += kIlp) {
         uint32_t rng[kIlp], best[kIlp], xpk[kIlp], qa[kIlp], qb[kIlp], qc[kIlp];   // rng ~0 = unknown
@@ -641,26 +644,34 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 #pragma unroll
         for (uint32_t u = 0; u < kIlp; u++) {
             const uint32_t x = xpk[u] & 0x1FFFu;
-            uint32_t st = 1, res = 0;
+            uint32_t res = 0;
             if (x < npos) {
                 const uint32_t Lb = best[u] >> 13, xb = 8191u - (best[u] & 0x1FFFu);
-                if (rng[u] == 0xFFFFFFFFu) { res = kUnknown; st = 0; s_unknown = 1; }
-                else if (Lb >= kMinL) { res = m_pack(Lb, x - xb); st = Lb + 1; }
+                if (rng[u] == 0xFFFFFFFFu) { res = kUnknown; s_unknown = 1; }
+                else if (Lb >= kMinL) { res = m_pack(Lb, x - xb); s_match = 1; }
             }
-            // the wave's 64 lanes hold 64 consecutive positions = one mbits word; m is
-            // stored (whole 256-B rows, zeros included) only by waves that found a match
-            const uint64_t mb = __ballot(res != 0);
-            if (mb && x < npos) m[bstart + w0 + x] = res;
-            if (mb && (tid & 63) == 0) s_match = 1;
-            const uint32_t xw = q0 + (tid & ~63u) + kMT * (g + u);
-            if ((tid & 63) == 0 && xw < npos) mbits[(uint64_t)b * L.wpb + ((w0 + xw) >> 6)] = mb;
-            const uint32_t q = g + u;
-            st_reg[q >> 1] = (q & 1) ? ((st_reg[q >> 1] & 0xFFFFu) | (st << 16)) : ((st_reg[q >> 1] & 0xFFFF0000u) | st);
+            rs[g + u] = res;
         }
     }
-    __syncthreads();   // the search region is dead from here on
+    __syncthreads();   // the search region is dead from here on; s_unknown is final
+    {
+        uint32_t *res_lds = region + kResLds;
+        const bool mfull = s_unknown != 0;
 #pragma unroll
-    for (uint32_t r = 0; r < kQPL; r++) step[tid + kMT * r] = (uint16_t)(st_reg[r >> 1] >> (16 * (r & 1)));
+        for (uint32_t r = 0; r < kQPL; r++) {
+            const uint32_t rel = tid + kMT * r, x = q0 + rel;
+            const uint32_t res = rs[r];
+            step[rel] = (uint16_t)(res == kUnknown ? 0u : m_len(res) + 1);
+            res_lds[rel] = res;
+            // the wave's 64 lanes hold 64 consecutive positions = one mbits word.  m rows
+            // (256 B, zeros included) go to HBM only where k_resolve / the stitch read them
+            // (the first kResolveSpan positions) or the tile needs the run table (all);
+            // every other match reaches k_emit through the tile's compact match list
+            const uint64_t mb = __ballot(res != 0);
+            if (mb && x < npos && (mfull || rel < kResolveSpan)) m[bstart + w0 + x] = res;
+            if ((tid & 63) == 0 && x < npos) mbits[(uint64_t)b * L.wpb + ((t0 + rel) >> 6)] = mb;
+        }
+    }
     __syncthreads();
     }   // bucket search
     }   // filter: sparse or bucket search
@@ -677,7 +688,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     const uint32_t nwords = (t1 - t0 + 63) / 64;
     if (s_unknown != 0) {
         for (uint32_t w = tid; w < nwords; w += kMT) cw[w] = 0;
-        if (tid == 0) { ti[0] = kTileLazy; ti[1] = 0; ti[2] = ti[3] = ti[4] = 0; }
+        if (tid == 0) { ti[0] = kTileLazy | kTileMFull; ti[1] = 0; ti[2] = ti[3] = ti[4] = 0; }
         return;
     }
 
@@ -772,6 +783,17 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         pre[q] = p + inc[q] - cnt[q];
         tot[q] = a;
     }
+    if (!dense) {
+        // compact match list: the speculative chain's match tokens in order (m values
+        // from the search results); with m rows only in the first kResolveSpan
+        // positions, k_emit takes the rest of the tile's matches from here
+        const uint32_t *res_lds = region + kResLds;
+        uint32_t *mt = mtok + (uint64_t)blockIdx.x * kTileMatches + pre[1];
+        for (uint32_t bits = T; bits; bits &= bits - 1) {
+            const uint32_t rel = s - t0 + __builtin_ctz(bits);
+            if (step[rel] > 1) *mt++ = res_lds[rel];
+        }
+    }
     constexpr uint32_t kLanesPerWord = 64 / kSeg;   // 8
     if ((tid % kLanesPerWord) == 0 && tid / kLanesPerWord < nwords) {
         const uint32_t w = tid / kLanesPerWord;
@@ -784,7 +806,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     if (tid == 0) {
         const uint32_t nsub = (t1 - t0 + kSeg - 1) / kSeg;
-        ti[0] = 0;
+        ti[0] = dense ? kTileMFull : 0u;   // dense: the run table wrote m for every position
         ti[1] = Gs[nsub];
         ti[2] = tot[0];
         ti[3] = tot[1];
@@ -793,14 +815,14 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 }
 
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
-                  uint32_t *tinfo, hipStream_t st, uint32_t dbg_override) {
+                  uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override) {
     // dbg bits exist only for fcx_debug_match (development; launches this kernel alone on
     // scratch the caller discards): bit0 skip searches, bit1 skip long extension, bit2 never /
     // bit3 always take the whole-tile run mode, bits 4-6 phase exits.  The product path
     // (fcx_compress_shard) always passes 0; nothing is read from the environment.
     const uint32_t dbg = dbg_override != ~0u ? dbg_override : 0u;
     const uint32_t grid = L.nblocks * L.tpb;
-    hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, dbg);
+    hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg);
 }
 
 }  // namespace fcx

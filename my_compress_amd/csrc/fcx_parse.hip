@@ -129,18 +129,41 @@ __device__ Cnt3 spec_prefix(const uint64_t *pfx, const uint32_t *mt, const uint6
     return c;
 }
 
+// the same counts for a tile whose m[] rows stop at kResolveSpan: the dropped
+// speculative match tokens are the first entries of the tile's compact match list
+// (k_match writes them in chain order), so their golomb bits come from there
+__device__ Cnt3 spec_prefix_c(const uint64_t *pfx, const uint32_t *mtt, const uint64_t *mb, uint64_t orig_word,
+                              uint32_t rel) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = rel >> 6, r = rel & 63;
+    const uint64_t p = pfx[w];
+    Cnt3 c{(uint32_t)(p & 0x1FFFu), (uint32_t)((p >> 13) & 0x7FFu), (uint32_t)((p >> 24) & 0x1FFFu)};
+    const uint64_t below = r ? (orig_word & ((1ull << r) - 1)) : 0ull;
+    const uint32_t nm = (uint32_t)__popcll(below & mb[w]);   // no unknowns: mbits = matches
+    uint32_t gb = 0;
+    if (lane < nm) {
+        const uint32_t L = m_len(mtt[c.mat + lane]);
+        gb = (L >> 2) + 3;
+    }
+    c.tok += (uint32_t)__popcll(below);
+    c.mat += nm;
+    c.gb += wave_sum_u32(gb);
+    return c;
+}
+
 // Fast-path resolution per tile, for all tiles in parallel ahead of the
 // sequential stitch.  Assume the true entry is the previous tile's speculative
 // exit (it is whenever the previous tile was resolved this way) and walk the
 // greedy chain from it until it meets this tile's speculative chain — usually
 // within a few tokens.  Recorded per tile (fp[8*tix]):
 //   [0] ok | rel << 1 (assumed entry - t0) | nmod << 16 (chain words rewritten)
-//   [1] tokens | matches << 32, [2] golomb bits (the tile's final counts)
+//   [1] tokens | matches << 32, [2] golomb bits | conv << 32 (the tile's final counts;
+//       conv = rel | dropped speculative matches << 16 where the walk met the
+//       speculative chain, kConvAll if it walked to the tile end)
 //   [3] exit (first chain position >= t1)
 //   [4..7] the rewritten chain words 0..3 (positions t0 .. t0+255)
 // ok = 0 when the walk needs > 256 positions, meets an unknown position, or a
 // neighbour is lazy: the stitch then walks the tile itself.
-constexpr uint32_t kResolveSpan = 256;
 
 __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__restrict__ m,
                                                 const uint64_t *__restrict__ mbits,
@@ -217,6 +240,7 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     }
     Cnt3 fin = walked;
     uint32_t keep_from = rel;   // speculative bits at positions >= keep_from stay
+    uint32_t convrec = kConvAll;
     if (conv) {
         const Cnt3 drop = rel ? spec_prefix(chain_pfx + (uint64_t)tix * (kTile / 64), mt, mb, orig[rel >> 6], rel)
                               : Cnt3{0, 0, 0};
@@ -224,6 +248,7 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
         fin.mat += ti[3] - drop.mat;
         fin.gb += ti[4] - drop.gb;
         exitv = ti[1];
+        convrec = rel | (drop.mat << 16);
     } else {
         keep_from = t1 - t0;   // the walk covered the rest of the tile
     }
@@ -241,7 +266,7 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
         }
         out[0] = 1ull | ((uint64_t)rel0 << 1) | ((uint64_t)nmod << 16);
         out[1] = (uint64_t)fin.tok | ((uint64_t)fin.mat << 32);
-        out[2] = fin.gb;
+        out[2] = fin.gb | ((uint64_t)convrec << 32);
         out[3] = exitv;
     }
     (void)conv;
@@ -250,10 +275,11 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
 __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                                const uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain, const uint64_t *__restrict__ chain_pfx,
                                                const uint32_t *__restrict__ tinfo, const uint64_t *__restrict__ fp,
-                                               uint32_t *__restrict__ tile_off, BlockInfo *__restrict__ binfo) {
+                                               const uint32_t *__restrict__ mtok, uint32_t *__restrict__ tile_off,
+                                               uint32_t *__restrict__ tconv, BlockInfo *__restrict__ binfo) {
     __shared__ uint32_t mL[kTile];
     __shared__ uint32_t sti[64][6];          // per tile of the batch: flags, exit, totals, k_resolve verdict
-    __shared__ uint32_t sfp[64][4];          // k_resolve: final counts, exit
+    __shared__ uint32_t sfp[64][5];          // k_resolve: final counts, exit, conv record
     __shared__ uint64_t sfw[64][4];          // k_resolve: rewritten chain words
     __shared__ uint64_t bmL[kTile / 64];
     __shared__ uint64_t mbL[kTile / 64];
@@ -285,13 +311,15 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 if (f0 & 1ull) {
                     const uint64_t f1 = fq[1];
                     sfp[lane][0] = (uint32_t)f1; sfp[lane][1] = (uint32_t)(f1 >> 32);
-                    sfp[lane][2] = (uint32_t)fq[2]; sfp[lane][3] = (uint32_t)fq[3];
+                    const uint64_t f2 = fq[2];
+                    sfp[lane][2] = (uint32_t)f2; sfp[lane][3] = (uint32_t)fq[3]; sfp[lane][4] = (uint32_t)(f2 >> 32);
                     for (uint32_t u = 0; u < 4; u++) sfw[lane][u] = fq[4 + u];
                 }
             }
             __syncthreads();
         }
         const bool lazy = (sti[j][0] & kTileLazy) != 0;
+        const bool mfull = (sti[j][0] & kTileMFull) != 0;   // else m[] rows stop at kResolveSpan
         uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
         const uint64_t *pfx = chain_pfx + (uint64_t)tix * (kTile / 64);
         const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
@@ -300,6 +328,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         if (lane < 3) tile_off[3 * tix + lane] = lane == 0 ? run.tok : lane == 1 ? run.mat : run.gb;
         if (e >= t1) {  // a match spans the whole tile
             for (uint32_t w = lane; w < nw; w += 64) cw[w] = 0;
+            if (lane == 0) tconv[tix] = kConvAll;
             continue;
         }
         const Cnt3 tot{sti[j][2], sti[j][3], sti[j][4]};
@@ -310,6 +339,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
             run.gb += sfp[j][2];
             const uint32_t nmod = fpv >> 16;
             if (lane < nmod) cw[lane] = sfw[j][lane];
+            if (lane == 0) tconv[tix] = mfull ? kConvAll : sfp[j][4];
             e = sfp[j][3];
             continue;
         }
@@ -333,23 +363,28 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 const uint32_t vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
                 for (uint32_t u = 0; u < 4; u++)
-                    if (x + u < nt) mL[x + u] = ((mbw >> u) & 1u) ? (x + 4 <= nt ? vv[u] : mt[x + u]) : 0u;
+                    if (x + u < nt)
+                        mL[x + u] = ((mbw >> u) & 1u) ? (mfull || x + u < kResolveSpan ? (x + 4 <= nt ? vv[u] : mt[x + u])
+                                                                                      : kUnknown)
+                                                      : 0u;
             }
         } else {
             for (uint32_t x = lane; x < nt; x += 64)   // m only where the position's mbits bit is set
-                mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? mt[x] : 0u;
+                mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? (mfull || x < kResolveSpan ? mt[x] : kUnknown) : 0u;
         }
         for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
         __syncthreads();
         if (e > t0) bm_apply(bmL, 0xFFFFFFFFu, 0, e - t0);
         __syncthreads();
-        uint32_t t = e, exitv;
+        uint32_t t = e, exitv, convrec = kConvAll;
         Cnt3 walked{0, 0, 0};
         for (;;) {
             const uint32_t rel = t - t0;
             if (!lazy && ((bmL[rel >> 6] >> (rel & 63)) & 1ull)) {
                 // converged: the speculative chain from here on is the true one
-                const Cnt3 drop = spec_prefix(pfx, mt, mb, cw[rel >> 6], rel);
+                const Cnt3 drop = mfull ? spec_prefix(pfx, mt, mb, cw[rel >> 6], rel)
+                                        : spec_prefix_c(pfx, mtok + (uint64_t)tix * kTileMatches, mb, cw[rel >> 6], rel);
+                if (!mfull) convrec = rel | (drop.mat << 16);
                 walked.tok += tot.tok - drop.tok;
                 walked.mat += tot.mat - drop.mat;
                 walked.gb += tot.gb - drop.gb;
@@ -378,6 +413,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         }
         __syncthreads();
         for (uint32_t w = lane; w < nw; w += 64) cw[w] = bmL[w];
+        if (lane == 0) tconv[tix] = convrec;
         __syncthreads();
         run.tok += walked.tok; run.mat += walked.mat; run.gb += walked.gb;
         e = exitv;
@@ -418,6 +454,18 @@ __device__ inline void block_scan3(uint32_t v[3], uint32_t tot[3], uint32_t *sh 
         v[q] = pre + inc[q] - v[q];
         tot[q] = all;
     }
+    __syncthreads();
+}
+
+// block-wide (256 threads) exclusive scan of one counter in place
+__device__ inline void block_scan1(uint32_t &v, uint32_t *sh /* >= 4 */) {
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) sh[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t w = 0; w < wv; w++) pre += sh[w];
+    v = pre + inc - v;
     __syncthreads();
 }
 
@@ -483,10 +531,11 @@ __device__ void emit_literal_tile(const uint8_t *d, const uint32_t *d32, uint64_
 
 __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
                                               const uint64_t *__restrict__ mbits, const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
-                                              const BlockInfo *__restrict__ binfo,
+                                              const BlockInfo *__restrict__ binfo, const uint32_t *__restrict__ mtok,
+                                              const uint32_t *__restrict__ tconv,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb) {
-    __shared__ uint32_t sh[12];
+    __shared__ uint32_t sh[16];
     __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW], lc[kCharW];
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
@@ -518,7 +567,19 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         const uint32_t valid = min(16u, t1 - s);
         if (valid < 16) bits &= (1u << valid) - 1;
     }
-    const uint32_t rd = bits & mbs;   // chain positions whose m is stored
+    // positions from the tile's conv point on (where the final chain joined the
+    // speculative one) take their matches from the compact list, in order; the others
+    // read m[] (first kResolveSpan positions, the stitch's walks, run-table tiles)
+    const uint32_t cv = tconv[blockIdx.x], crel = cv & 0xFFFFu;   // conv rel | dropped speculative matches << 16
+    uint32_t post = 0;
+    if (crel != kConvAll) {
+        const uint32_t rel0 = s - t0;
+        post = rel0 >= crel ? 0xFFFFu : rel0 + 16 > crel ? (0xFFFFu << (crel - rel0)) & 0xFFFFu : 0u;
+    }
+    const uint32_t rd = bits & mbs & ~post;   // chain positions whose m is in m[]
+    const uint32_t rc = bits & mbs & post;    // chain matches in the compact list
+    uint32_t cbase = (uint32_t)__builtin_popcount(rc);
+    block_scan1(cbase, sh + 12);
     const uint32_t *mt = m + bstart + s;
     uint32_t mm[16];
     uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0};
@@ -532,9 +593,12 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
 #pragma unroll
         for (uint32_t q = 0; q < 16; q++) mm[q] = ((rd >> q) & 1u) ? mt[q] : 0u;
     }
+    // the list starts at the tile's first speculative position: skip the matches the
+    // final chain dropped before the conv point
+    const uint32_t *mct = mtok + (uint64_t)blockIdx.x * kTileMatches + (cv >> 16) + cbase;
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
-        mm[q] = ((rd >> q) & 1u) ? mm[q] : 0u;
+        mm[q] = ((rd >> q) & 1u) ? mm[q] : ((rc >> q) & 1u) ? *mct++ : 0u;
         const uint32_t Lq = m_len(mm[q]);
         if (((bits >> q) & 1u) && Lq) { v[1]++; v[2] += (Lq >> 2) + 3; }
     }
@@ -641,16 +705,16 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
 }
 
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
-                  const uint64_t *chain_pfx,
-                  const uint32_t *tinfo, uint64_t *fp, uint32_t *tile_off, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
+                  const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
+                  uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
                   uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev) {
     const uint32_t ntiles = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_resolve, dim3(ntiles), dim3(64), 0, st, L, m, mbits, chain, chain_pfx, tinfo, fp);
-    hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, tile_off,
-                       binfo);
+    hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, mtok,
+                       tile_off, tconv, binfo);
     if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, s_flags,
-                       s_chars, s_p, s_golomb);
+    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok, tconv,
+                       s_flags, s_chars, s_p, s_golomb);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 
