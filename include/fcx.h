@@ -16,6 +16,10 @@
  *                            per record                                            :4160-4204, :2255
  *                            (GPU decoder: every record of a device-resident run)
  *   fcx_decompress_host   <- the whole decompress mode of main() on host buffers  :4137-4204
+ *   fcx_dist_*            <- main()'s compress loop (:4090-4122) with the blocks spread over
+ *                            several GPUs: contiguous block ranges per GPU, the segments
+ *                            concatenated in block order over RCCL (the reference writes the
+ *                            blocks to one file in order, :4112-4114)
  *
  * Conventions: plain pointers and sizes, no exceptions cross the ABI, every
  * function returns FCX_OK (0) or a negative FCX_ERR_* code unless stated; the
@@ -41,6 +45,7 @@ extern "C" {
 #define FCX_ERR_FORMAT (-4)    /* malformed compressed stream */
 #define FCX_ERR_INTERNAL (-5)  /* device-side invariant violated */
 #define FCX_ERR_NOMEM (-6)
+#define FCX_ERR_RCCL (-7)      /* RCCL (collective) error */
 
 #define FCX_HEADER_BYTES 10u                 /* "FCX7" + u32 total + u16 blocks (:101-109) */
 #define FCX_DEFAULT_BLOCK_BYTES (1u << 20)  /* BLOCK_BYTES (:113) */
@@ -192,6 +197,45 @@ uint32_t fcx_lz78_compress_block(const void *in, uint32_t len, uint8_t *out);
  * zeros).  decompress_block returns decoded bytes or a negative FCX_ERR_*. */
 int64_t fcx_lz78_decompress_block(const uint8_t *in, uint32_t len, uint8_t *out, uint64_t cap);
 int fcx_lz78_decompress_host(const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t cap, uint64_t *out_len);
+
+/* ---- multi-GPU: block ranges per GPU + RCCL over xGMI -------------------------
+ * Blocks are independent (the window and the parse restart per block, :1675-1703), so
+ * rank r of N compresses the contiguous block range fcx_dist_block_range(nb, r, N) of the
+ * input and the only exchange is the concatenation of the per-rank segments
+ * ([u32 len][payload]... each) in rank order: an all-gather of the u64 segment sizes,
+ * then either a gather to rank 0 (grouped point-to-point receives, every xGMI link at
+ * once, 1/N of the all-gather's traffic) or an all-gather-v (one broadcast per source
+ * rank with its exact size), straight into the output buffer at each segment's offset.
+ * The 10-byte header is the caller's (fcx_write_header from the global totals). */
+typedef struct fcx_dist fcx_dist;
+#define FCX_DIST_ID_BYTES 128u   /* ncclUniqueId */
+#define FCX_DIST_GATHER 0        /* concat to rank 0 only */
+#define FCX_DIST_ALLGATHER 1     /* concat on every rank */
+
+/* contiguous block range [b0, b1) of rank r of n (the partition of my_compress_amd.dist) */
+void fcx_dist_block_range(uint64_t nblocks, int rank, int nranks, uint64_t *b0, uint64_t *b1);
+/* a fresh RCCL unique id (rank 0 creates it; the caller hands it to every rank) */
+int fcx_dist_unique_id(uint8_t *id);
+/* one rank of an N-process job (one process per GPU, on HIP device `device`) */
+int fcx_dist_init_rank(fcx_dist **d, int nranks, int rank, const uint8_t *id, int device);
+/* one process driving ndev devices (rank i on devices[i]; ncclCommInitAll) */
+int fcx_dist_init_local(fcx_dist **d, int ndev, const int *devices);
+void fcx_dist_destroy(fcx_dist *d);
+/* ranks of the job and ranks driven by this process */
+int fcx_dist_size(fcx_dist *d, int *nranks, int *nlocal);
+/* Concatenates the segments of every rank in rank order (process-per-GPU form: local
+ * index 0).  d_seg/seg_len: this rank's segment (device); d_out/cap: the destination
+ * (device; on rank 0 for FCX_DIST_GATHER it may be the buffer d_seg lives in, with
+ * d_seg == d_out).  *total receives the concatenated length on every rank.  Enqueued on
+ * `stream` (a hipStream_t of the rank's device) and synchronised. */
+int fcx_dist_concat(fcx_dist *d, int local, const uint8_t *d_seg, uint64_t seg_len, uint8_t *d_out, uint64_t cap,
+                    uint64_t *total, int mode, void *stream);
+/* The whole job in one process (fcx_dist_init_local): host input, rounds of up to
+ * round_bytes per device (0 = 1 GiB) split into block ranges, every device compresses
+ * its range with one host thread each, the segments are gathered to local rank 0 over
+ * RCCL and copied to `out` ([u32 len][payload] records, no header); *out_len = bytes. */
+int fcx_dist_compress_host(fcx_dist *d, const uint8_t *in, uint64_t n, uint32_t block_bytes, uint64_t round_bytes,
+                           uint8_t *out, uint64_t cap, uint64_t *out_len);
 
 const char *fcx_last_error(void);
 const char *fcx_version(void);

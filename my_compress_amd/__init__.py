@@ -101,6 +101,19 @@ def lib():
     L.fcx_lz78_decompress_block.restype = ctypes.c_int64
     L.fcx_lz78_decompress_host.argtypes = [c_u8p, ctypes.c_uint64, c_u8p, ctypes.c_uint64,
                                            ctypes.POINTER(ctypes.c_uint64)]
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    L.fcx_dist_block_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P64, P64]
+    L.fcx_dist_block_range.restype = None
+    L.fcx_dist_unique_id.argtypes = [c_u8p]
+    L.fcx_dist_init_rank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, c_u8p, ctypes.c_int]
+    L.fcx_dist_init_local.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.fcx_dist_destroy.argtypes = [ctypes.c_void_p]
+    L.fcx_dist_destroy.restype = None
+    L.fcx_dist_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.fcx_dist_concat.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_uint64, P64, ctypes.c_int, ctypes.c_void_p]
+    L.fcx_dist_compress_host.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                         c_u8p, ctypes.c_uint64, P64]
     L.fcx_last_error.restype = ctypes.c_char_p
     L.fcx_version.restype = ctypes.c_char_p
     _lib = L
@@ -388,3 +401,75 @@ def decompress_lz78(blob: bytes, cap: int = None) -> bytes:
 def lz78_release() -> None:
     """frees the LZ78 compress scratch cached on the current HIP device"""
     _check(lib().fcx_lz78_release(), "fcx_lz78_release")
+
+
+# ---- multi-GPU (fcx_dist_*: block ranges per GPU, RCCL concatenation) ----------------
+DIST_GATHER, DIST_ALLGATHER = 0, 1
+
+
+def dist_block_range(nblocks: int, rank: int, nranks: int):
+    """the C partition (fcx_dist_block_range); equals my_compress_amd.dist.block_range"""
+    b0, b1 = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().fcx_dist_block_range(nblocks, rank, nranks, ctypes.byref(b0), ctypes.byref(b1))
+    return b0.value, b1.value
+
+
+def dist_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().fcx_dist_unique_id(buf), "fcx_dist_unique_id")
+    return buf.raw
+
+
+class Dist:
+    """fcx_dist: RCCL communicator(s) of the multi-GPU compress path.
+    Dist.local([0, 1, ...]) drives several devices from this process (the CLI's -g N);
+    Dist.rank(n, r, uid, device) is one rank of a process-per-GPU job."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def local(cls, devices):
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_int * len(devices))(*devices)
+        _check(lib().fcx_dist_init_local(ctypes.byref(h), len(devices), arr), "fcx_dist_init_local")
+        return cls(h)
+
+    @classmethod
+    def rank(cls, nranks: int, rank: int, uid: bytes, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().fcx_dist_init_rank(ctypes.byref(h), nranks, rank, uid, device), "fcx_dist_init_rank")
+        return cls(h)
+
+    def close(self):
+        if self._h:
+            lib().fcx_dist_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self):
+        n, loc = ctypes.c_int(), ctypes.c_int()
+        _check(lib().fcx_dist_size(self._h, ctypes.byref(n), ctypes.byref(loc)), "fcx_dist_size")
+        return n.value, loc.value
+
+    def concat(self, d_seg: int, seg_len: int, d_out: int, cap: int, mode: int = DIST_GATHER, stream: int = 0) -> int:
+        """this rank's device segment -> the concatenation in rank order at d_out; returns its length"""
+        tot = ctypes.c_uint64()
+        _check(lib().fcx_dist_concat(self._h, 0, ctypes.c_void_p(d_seg), seg_len, ctypes.c_void_p(d_out), cap,
+                                     ctypes.byref(tot), mode, ctypes.c_void_p(stream)), "fcx_dist_concat")
+        return tot.value
+
+    def compress_host(self, data: bytes, block_bytes: int = BLOCK_BYTES, round_bytes: int = 0) -> bytes:
+        """records ([u32 len][payload]...) of data, block ranges over this process's devices"""
+        cap = shard_bound(len(data), block_bytes)
+        out = ctypes.create_string_buffer(max(cap, 1))
+        got = ctypes.c_uint64()
+        _check(lib().fcx_dist_compress_host(self._h, data, len(data), block_bytes, round_bytes, out, cap,
+                                            ctypes.byref(got)), "fcx_dist_compress_host")
+        return out.raw[:got.value]
+

@@ -9,7 +9,9 @@
 // fcx_decompress_stream: file reads and writes overlap the device work); without
 // a HIP device, compress fails and decompress uses the host decoder.  Superset:
 // -b/--block BYTES (<= 1 MiB; the reference fixes 1 MiB, BLOCK_BYTES :113) and
-// -d/--device N.  `-c lz78` runs the LZ78 codec (FCX8) on the GPU: 256 MiB shards
+// -d/--device N and -g/--gpus N (-c lz77 over N GPUs of this node, devices d .. d+N-1:
+// contiguous block ranges per GPU, segments gathered over RCCL, byte-identical
+// output).  `-c lz78` runs the LZ78 codec (FCX8) on the GPU: 256 MiB shards
 // through fcx_lz78_compress_host / fcx_lz78_decompress_host (whole files in host
 // memory for decompress).
 #include <getopt.h>
@@ -28,7 +30,8 @@
 static int usage() {
     fprintf(stderr,
             "usage: ./my_compress -i[or --file_in] <input file name> [-o[or --file_out] <output file name>] "
-            "[-c (or --compress) <lz77/lz78>] [-b (or --block) <bytes>] [-d (or --device) <hip device>]\n");
+            "[-c (or --compress) <lz77/lz78>] [-b (or --block) <bytes>] [-d (or --device) <hip device>] "
+            "[-g (or --gpus) <count>]\n");
     return -1;
 }
 
@@ -78,6 +81,54 @@ static int do_compress(FILE *fin, FILE *fout, uint32_t block, int device) {
     if (nblocks > 65535) fprintf(stderr, "warning: %llu blocks exceed the u16 block count of the format\n",
                                  (unsigned long long)nblocks);
     fcx_ctx_destroy(ctx);
+    return 0;
+}
+
+// -c lz77 over ngpus devices (fcx_dist_compress_host): the file in rounds of up to
+// 1 GiB per GPU, each round's block ranges compressed in parallel and gathered to the
+// first device over RCCL, records written in block order (4090-4122)
+static int do_compress_dist(FILE *fin, FILE *fout, uint32_t block, int device, int ngpus) {
+    std::vector<int> devs(ngpus);
+    for (int i = 0; i < ngpus; i++) devs[i] = device + i;
+    fcx_dist *d = nullptr;
+    if (fcx_dist_init_local(&d, ngpus, devs.data())) {
+        fprintf(stderr, "fcx: %s\n", fcx_last_error());
+        return -1;
+    }
+    const uint64_t per = (1ull << 30) / block * block;
+    std::vector<uint8_t> buf(per * (uint64_t)ngpus), out(fcx_shard_bound(buf.size(), block));
+    uint8_t hdr[FCX_HEADER_BYTES];
+    fcx_write_header(hdr, 0, 0);
+    fwrite(hdr, 1, sizeof(hdr), fout);
+    uint64_t total_in = 0, total_out = 0, nblocks = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = 0;
+    for (;;) {
+        const size_t n = fread(buf.data(), 1, buf.size(), fin);
+        if (n == 0) break;
+        uint64_t got = 0;
+        if (fcx_dist_compress_host(d, buf.data(), n, block, per, out.data(), out.size(), &got)) {
+            fprintf(stderr, "fcx: %s\n", fcx_last_error());
+            rc = -1;
+            break;
+        }
+        fwrite(out.data(), 1, (size_t)got, fout);
+        total_in += n;
+        total_out += got;
+        nblocks += (n + block - 1) / block;
+    }
+    fcx_dist_destroy(d);
+    if (rc) return rc;
+    fcx_write_header(hdr, total_in, nblocks);
+    fseek(fout, 0, SEEK_SET);
+    fwrite(hdr, 1, sizeof(hdr), fout);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    printf("<Final>: LZ77 totalBytes = %llu, compress total bytes=%llu, compress rate: %.2f%% (%d GPUs)\n",
+           (unsigned long long)total_in, (unsigned long long)total_out,
+           total_in ? 100.0 * (double)total_out / (double)total_in : 0.0, ngpus);
+    printf("[***TIME***]  All block compress spend %.0f ms!!!\n", ms);
+    if (nblocks > 65535) fprintf(stderr, "warning: %llu blocks exceed the u16 block count of the format\n",
+                                 (unsigned long long)nblocks);
     return 0;
 }
 
@@ -204,13 +255,15 @@ int main(int argc, char **argv) {
                                            {"compress", required_argument, nullptr, 'c'},
                                            {"block", required_argument, nullptr, 'b'},
                                            {"device", required_argument, nullptr, 'd'},
+                                           {"gpus", required_argument, nullptr, 'g'},
                                            {nullptr, 0, nullptr, 0}};
     std::string file_in, file_out = "./out";
     bool compress = false, lz77 = false;
     uint32_t block = FCX_DEFAULT_BLOCK_BYTES;
-    int device = 0, opt;
+    int device = 0, ngpus = 1, opt;
+    bool dist = false;   // -g given: the RCCL multi-GPU path (also at -g 1)
     if (argc < 3) return usage();
-    while ((opt = getopt_long(argc, argv, "i:o:c:b:d:", long_options, nullptr)) != -1) {
+    while ((opt = getopt_long(argc, argv, "i:o:c:b:d:g:", long_options, nullptr)) != -1) {
         switch (opt) {
         case 'i': file_in = optarg; break;
         case 'o': file_out = optarg; break;
@@ -220,10 +273,11 @@ int main(int argc, char **argv) {
             break;
         case 'b': block = (uint32_t)strtoul(optarg, nullptr, 0); break;
         case 'd': device = atoi(optarg); break;
+        case 'g': ngpus = atoi(optarg); dist = true; break;
         default: return usage();
         }
     }
-    if (file_in.empty()) return usage();
+    if (file_in.empty() || ngpus < 1) return usage();
     if (block == 0 || block > FCX_MAX_BLOCK_BYTES) {
         fprintf(stderr, "block size must be in [1, %u]\n", FCX_MAX_BLOCK_BYTES);
         return -1;
@@ -237,7 +291,9 @@ int main(int argc, char **argv) {
         fprintf(stderr, "fcx: no HIP device %d\n", device);
         return -1;
     }
-    const int r = compress ? (lz77 ? do_compress(fin, fout, block, device) : compress_lz78(fin, fout, block))
+    const int r = compress ? (lz77 ? (dist ? do_compress_dist(fin, fout, block, device, ngpus)
+                                                                  : do_compress(fin, fout, block, device))
+                                   : compress_lz78(fin, fout, block))
                            : do_decompress(fin, fout, device);
     fclose(fin);
     fclose(fout);

@@ -81,3 +81,25 @@ def test_block_ranges_partition():
             assert rs[0][0] == 0 and rs[-1][1] == nb
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
             assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+def test_c_partition_matches_python():
+    """fcx_dist_block_range (C, the CLI's -g N and fcx_dist_compress_host) and
+    my_compress_amd.dist.block_range (the Python ranks) split identically"""
+    import my_compress_amd as mc
+
+    for nb in [0, 1, 2, 5, 8, 1023, 1024, 8192, 65535]:
+        for world in [1, 2, 3, 4, 7, 8]:
+            for r in range(world):
+                assert mc.dist_block_range(nb, r, world) == fdist.block_range(nb, r, world)
+
+
+def test_dist_needs_a_gpu_without_one():
+    import torch
+
+    import my_compress_amd as mc
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(mc.FcxError):
+        mc.Dist.local([0])
