@@ -138,7 +138,7 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     if world == 1 and args.host_path and main_leg:
         host_path = host_leg(host, n, block)
     del host
-    concat = args.concat if world > 1 else "none"
+    concat = args.concat if dist else "none"
     # gather: rank 0's compress output buffer is also the file buffer (its segment sits at offset 0)
     cap = mc.shard_bound(n_global if (concat == "gather" and rank == 0) else n, block)
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
@@ -158,6 +158,14 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
         seg_len = ctx.read_out_len() if n else 0
         if concat == "none":
             state["total"] = seg_len
+            return
+        if args.fcx_dist is not None:   # C++ RCCL path: sizes all-gather + gather / all-gather-v
+            import my_compress_amd as mc2
+
+            dst = d_out if concat == "gather" else whole
+            mode = mc2.DIST_GATHER if concat == "gather" else mc2.DIST_ALLGATHER
+            state["total"] = args.fcx_dist.concat(d_out.data_ptr(), seg_len, dst.data_ptr(), dst.numel(), mode, sid)
+            state["seg"] = seg_len
             return
         sizes, offs = fdist.exchange_sizes(seg_len, dist, dev if dist.get_backend() != "gloo" else "cpu")
         seg = d_out[:seg_len]
@@ -206,6 +214,8 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     }
     if concat != "none":
         res["concat_ms_per_step"] = res["ms_per_step"] - res["compress_only"]["ms_per_step"]
+        res["concat_impl"] = "fcx_dist (C++ RCCL)" if args.fcx_dist is not None else \
+            f"torch.distributed ({dist.get_backend()})"
     stats = ctx.stats() if n else {"tokens": 0, "matches": 0, "lazy_evals": 0, "lazy_tiles": 0}
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
@@ -501,7 +511,11 @@ def main():
                     help="extra legs after the main one (comma list of " + ",".join(LEGS) + ")")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling (config 4) leg at N > 1")
     ap.add_argument("--concat", default="gather", choices=["gather", "allgather", "none"])
+    ap.add_argument("--concat-impl", default="fcx", choices=["fcx", "torch"],
+                    help="fcx: the C++ RCCL path (fcx_dist_concat); torch: torch.distributed P2P / broadcast")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--dist-rehearsal", action="store_true",
+                    help="use the multi-rank code path (process group, concatenation) even at N=1 (under torchrun)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the GPU decoder timing")
     ap.add_argument("--no-host-path", dest="host_path", action="store_false",
@@ -520,7 +534,7 @@ def main():
     dev = torch.device("cuda:0" if os.environ.get("FCX_BENCH_SAME_DEVICE") == "1" else f"cuda:{local}")
     torch.cuda.set_device(dev)
     dist = None
-    if world > 1:
+    if world > 1 or args.dist_rehearsal:
         import torch.distributed as dist_
 
         if args.dist_backend == "nccl":
@@ -528,6 +542,17 @@ def main():
         else:
             dist_.init_process_group("gloo")
         dist = dist_
+    args.fcx_dist = None
+    if dist and args.dist_backend == "nccl" and args.concat_impl == "fcx":
+        # the C++ RCCL communicator of the concatenation (fcx_dist_init_rank); its unique id
+        # travels over the torch process group
+        import my_compress_amd as mc
+
+        uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(mc.dist_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        args.fcx_dist = mc.Dist.rank(world, rank, bytes(uid.cpu().numpy().tobytes()), dev.index)
     main_res = run_leg(args.kind, SEEDS[args.kind], args.block, args, rank, world, dev, dist, True,
                        scaling=args.scaling, main_leg=True)
     legs = {}
@@ -537,7 +562,7 @@ def main():
             continue
         legs[name] = run_leg(kind, SEEDS[kind], block, args, rank, world, dev, dist, True)
     weak = None
-    if world > 1 and not args.no_weak and args.scaling == "strong":
+    if dist and not args.no_weak and args.scaling == "strong":
         weak = run_leg("rand", 4, 1 << 20, args, rank, world, dev, dist, False, scaling="weak")
 
     if rank == 0:
@@ -584,6 +609,7 @@ def main():
             "bit_exact_vs_reference": main_res.get("bit_exact_vs_reference"),
             "compress_only": main_res["compress_only"],
             "concat_ms_per_step": main_res.get("concat_ms_per_step"),
+            "concat_impl": main_res.get("concat_impl"),
             "stages_ms": main_res["stages_ms"],
             "lazy_evals": main_res["lazy_evals"],
             "decode": main_res.get("decode"),
@@ -602,6 +628,8 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()
+        if args.fcx_dist is not None:
+            args.fcx_dist.close()
         dist.destroy_process_group()
 
 
