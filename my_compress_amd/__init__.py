@@ -373,8 +373,11 @@ def compress_lz78(data: bytes, block_bytes: int = BLOCK_BYTES) -> bytes:
     cap = lz78_bound(len(data), block_bytes)
     out = ctypes.create_string_buffer(cap)
     n = ctypes.c_uint64()
-    _check(lib().fcx_lz78_compress_host(data, len(data), block_bytes, out, cap, ctypes.byref(n)),
-           "fcx_lz78_compress_host")
+    try:
+        _check(lib().fcx_lz78_compress_host(data, len(data), block_bytes, out, cap, ctypes.byref(n)),
+               "fcx_lz78_compress_host")
+    finally:
+        lib().fcx_lz78_release()   # the codec caches ~40 B of device scratch per input byte
     return out.raw[:n.value]
 
 
@@ -389,13 +392,18 @@ def my_decompress_file_lz78(payload: bytes, cap: int = BLOCK_BYTES + 8) -> bytes
 
 def decompress_lz78(blob: bytes, cap: int = None) -> bytes:
     """whole FCX8 file -> bytes on the GPU (main() decompress mode, :4137-4204)"""
-    if cap is None:
-        nb = struct.unpack_from("<H", blob, 8)[0] if len(blob) >= HEADER_BYTES else 0
-        cap = nb * (BLOCK_BYTES + 8)
-    out = ctypes.create_string_buffer(max(cap, 1))
-    n = ctypes.c_uint64()
-    _check(lib().fcx_lz78_decompress_host(blob, len(blob), out, cap, ctypes.byref(n)), "fcx_lz78_decompress_host")
-    return out.raw[:n.value]
+    caps = [cap]
+    if cap is None:   # the header's total (+ slack), then the per-block bound if the total wrapped
+        total, nb = struct.unpack_from("<IH", blob, 4) if len(blob) >= HEADER_BYTES else (0, 0)
+        caps = [total + 64 * nb + 64, nb * (BLOCK_BYTES + 8) + 1]
+    for i, c in enumerate(caps):
+        out = ctypes.create_string_buffer(max(c, 1))
+        n = ctypes.c_uint64()
+        rc = lib().fcx_lz78_decompress_host(blob, len(blob), out, c, ctypes.byref(n))
+        if rc == -2 and i + 1 < len(caps):   # FCX_ERR_CAPACITY
+            continue
+        _check(rc, "fcx_lz78_decompress_host")
+        return out.raw[:n.value]
 
 
 def lz78_release() -> None:

@@ -195,6 +195,9 @@ static int compress_lz78(FILE *fin, FILE *fout, uint32_t block) {
            (unsigned long long)total_in, (unsigned long long)total_out,
            total_in ? 100.0 * (double)total_out / (double)total_in : 0.0);
     printf("[***TIME***]  All block compress spend %.0f ms!!!\n", ms);
+    if (nblocks > 65535) fprintf(stderr, "warning: %llu blocks exceed the u16 block count of the format\n",
+                                 (unsigned long long)nblocks);
+    (void)fcx_lz78_release();   // the codec's cached device scratch
     return 0;
 }
 
@@ -206,9 +209,17 @@ static int decompress_lz78(FILE *fin, FILE *fout, uint32_t total) {
     while ((n = fread(tmp, 1, sizeof(tmp), fin)) > 0) blob.insert(blob.end(), tmp, tmp + n);
     uint16_t nblocks;
     memcpy(&nblocks, blob.data() + 8, 2);
-    std::vector<uint8_t> out((uint64_t)nblocks * (FCX_MAX_BLOCK_BYTES + 8) + 1);
+    // decoded bytes <= the header's total (mod 2^32; the reference decoder never adds
+    // bytes, it may drop a trailing 0x00 per block): size by it, and only when that
+    // fails on capacity (a total that wrapped) by the decoder's per-block bound (:2373)
+    std::vector<uint8_t> out((uint64_t)total + 64ull * nblocks + 64);
     uint64_t got = 0;
-    if (fcx_lz78_decompress_host(blob.data(), blob.size(), out.data(), out.size(), &got)) {
+    int r = fcx_lz78_decompress_host(blob.data(), blob.size(), out.data(), out.size(), &got);
+    if (r == FCX_ERR_CAPACITY) {
+        out.assign((uint64_t)nblocks * (FCX_MAX_BLOCK_BYTES + 8) + 1, 0);
+        r = fcx_lz78_decompress_host(blob.data(), blob.size(), out.data(), out.size(), &got);
+    }
+    if (r) {
         fprintf(stderr, "fcx: %s\n", fcx_last_error());
         return -1;
     }

@@ -37,8 +37,9 @@
 namespace fcx78 {
 
 constexpr uint32_t kTileTok = 8192;   // tokens per pack tile (256 lanes x 32)
-constexpr uint32_t kSortCap = 8192;
-constexpr uint32_t kGroupLds = 4112;  // >= groups of a 1 MiB block (ceil((2^20 + 1) / 256))   // bitonic sort capacity (>= max group count 4097)
+constexpr uint32_t kSortCap = 8192;   // bitonic sort capacity (>= the max group count 4097 of a 1 MiB block)
+constexpr uint32_t kGroupLds = 4112;  // LDS group counters: >= groups of a 1 MiB block, ceil((2^20 + 1) / 256)
+static_assert(kGroupLds >= FCX_MAX_BLOCK_BYTES / 256 + 1 && kSortCap >= FCX_MAX_BLOCK_BYTES / 256 + 1, "group capacity");
 
 struct Rec78 {
     uint32_t N, maxi, wcnt, G;
@@ -1122,6 +1123,10 @@ int fcx_lz78_decompress_host(const uint8_t *in, uint64_t in_len, uint8_t *out, u
         rlen.push_back(sz);
         q += sz;
     }
+    // the u16 block count wraps past 65535 blocks (:105): records the header does not
+    // count would be dropped silently, so they are an error here
+    if (q != in_len)
+        return fail78(FCX_ERR_FORMAT, "fcx_lz78: bytes after the last counted record (more than 65535 blocks?)");
     return lz78_decode_records(in, in_len, roff, rlen, out, cap, out_len);
 }
 

@@ -89,6 +89,20 @@ def test_cli_lz78_matches_oracle_and_round_trips(tmp_path):
     assert (tmp_path / "back").read_bytes() == oracle.lz78_decompress_file((tmp_path / "c8").read_bytes(), len(data) + 64)
 
 
+@pytest.mark.gpu
+def test_cli_lz78_small_blocks_round_trip(tmp_path):
+    """-c lz78 -b 4096 on ~3 MiB (770 blocks): the decompress buffer follows the header's
+    total, not 1 MiB per block"""
+    data = inputs.mosaic(43, (3 << 20) + 17)
+    (tmp_path / "plain").write_bytes(data)
+    r = run(["-i", "plain", "-o", "c8", "-c", "lz78", "-b", "4096"], tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert (tmp_path / "c8").read_bytes() == oracle.lz78_compress_file(data, 4096)
+    r = run(["-i", "c8", "-o", "back"], tmp_path)   # FAIL on size is the reference's verdict when
+    assert "decompress total bytes" in r.stdout, r.stderr   # blocks end in 0x00 (3701-3703)
+    assert (tmp_path / "back").read_bytes() == oracle.lz78_decompress_file((tmp_path / "c8").read_bytes(), len(data) + 64 * 800)
+
+
 def test_cli_compress_fails_loudly_without_gpu(tmp_path):
     if gpu_present():
         pytest.skip("GPU present")
