@@ -457,15 +457,20 @@ __device__ inline void block_scan3(uint32_t v[3], uint32_t tot[3], uint32_t *sh 
     __syncthreads();
 }
 
-// block-wide (256 threads) exclusive scan of one counter in place
-__device__ inline void block_scan1(uint32_t &v, uint32_t *sh /* >= 4 */) {
+// block-wide (256 threads) exclusive scan of one counter in place, with the total
+__device__ inline void block_scan1t(uint32_t &v, uint32_t &total, uint32_t *sh /* >= 4 */) {
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const uint32_t inc = wave_incl_scan(v);
     if (lane == 63) sh[wv] = inc;
     __syncthreads();
-    uint32_t pre = 0;
-    for (uint32_t w = 0; w < wv; w++) pre += sh[w];
+    uint32_t pre = 0, all = 0;
+    for (uint32_t w = 0; w < 4; w++) {
+        const uint32_t x = sh[w];
+        if (w < wv) pre += x;
+        all += x;
+    }
     v = pre + inc - v;
+    total = all;
     __syncthreads();
 }
 
@@ -497,30 +502,23 @@ __device__ inline void flush_words(uint32_t *g, uint32_t gw0, const uint32_t *w,
     }
 }
 
-// all-literal tile (random data): the tile's chars are its input bytes, its flags all
-// ones; copied at the tile's unaligned stream offsets without staging
-__device__ void emit_literal_tile(const uint8_t *d, const uint32_t *d32, uint64_t avail, uint32_t t0, uint32_t nt,
-                                  uint32_t tok0, uint8_t *chars, uint32_t *flags) {
+// all-literal tile (random data): the tile's chars are its input bytes (staged in LDS),
+// its flags all ones; output dwords on the stream's dword grid by alignbyte, the
+// partial dwords at the tile's two ends as byte stores
+__device__ void emit_literal_tile(const uint32_t *lin, uint32_t nt, uint32_t tok0, uint8_t *chars, uint32_t *flags) {
     const uint32_t tid = threadIdx.x;
-    const uint32_t a = (tok0 + 3) & ~3u, z = (tok0 + nt) & ~3u;   // [a, z): whole output dwords
-    const uint32_t sh = (t0 - tok0) & 3u;
-    for (uint32_t q = (a >> 2) + tid; q < (z >> 2); q += 256) {
-        const uint32_t so = t0 + 4 * q - tok0;   // input byte of output byte 4q
-        const uint32_t wi = so >> 2;
-        const uint32_t lo = d32[wi];
-        uint32_t v = lo;
-        if (sh) {
-            uint32_t hi = 0;
-            if (4ull * wi + 8 <= avail) hi = d32[wi + 1];
-            else
-                for (uint32_t j = 0; j < 4 && 4ull * wi + 4 + j < avail; j++) hi |= (uint32_t)d[4 * wi + 4 + j] << (8 * j);
-            v = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        }
-        ((uint32_t *)chars)[q] = v;
+    const uint8_t *lb = (const uint8_t *)lin;
+    const uint32_t e = (4u - (tok0 & 3u)) & 3u;             // input byte of the first whole output dword
+    const uint32_t nfull = nt >= e ? (nt - e) >> 2 : 0u;      // whole output dwords
+    uint32_t *c4 = (uint32_t *)chars + ((tok0 + e) >> 2);
+#pragma unroll
+    for (uint32_t u = 0; u < kTile / 4 / 256; u++) {
+        const uint32_t j = tid + 256 * u;
+        if (j < nfull) c4[j] = __builtin_amdgcn_alignbyte(lin[j + 1], lin[j], e);
     }
-    const uint32_t head_end = min(a, tok0 + nt);
-    if (tid < head_end - tok0) chars[tok0 + tid] = d[t0 + tid];
-    if (z >= a && tid < tok0 + nt - z) chars[z + tid] = d[t0 + z - tok0 + tid];
+    const uint32_t zf = e + 4 * nfull;
+    if (tid < min(e, nt)) chars[tok0 + tid] = lb[tid];
+    if (tid < nt - min(zf, nt)) chars[tok0 + zf + tid] = lb[zf + tid];
     const uint32_t f0 = tok0, f1 = tok0 + nt;
     for (uint32_t w = (f0 >> 5) + tid; w <= ((f1 - 1) >> 5); w += 256) {
         const uint32_t lo = max(f0, 32 * w), hi = min(f1, 32 * w + 32);
@@ -529,6 +527,12 @@ __device__ void emit_literal_tile(const uint8_t *d, const uint32_t *d32, uint64_
     }
 }
 
+constexpr uint32_t kInW = (kTile + kLookAhead) / 4 + 2;   // tile input + look-ahead (dwords)
+
+// Latency shape: every load that does not depend on another goes out first (tile
+// offsets, conv record, chain and mbits words, the tile's input + look-ahead into LDS);
+// after one block scan, the second and last round of loads (m rows, the compact match
+// list into LDS); everything after that is LDS work and stores.
 __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
                                               const uint64_t *__restrict__ mbits, const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
                                               const BlockInfo *__restrict__ binfo, const uint32_t *__restrict__ mtok,
@@ -537,6 +541,8 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb) {
     __shared__ uint32_t sh[16];
     __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW], lc[kCharW];
+    __shared__ uint32_t lin[kInW];           // input bytes [t0, t0 + kTile + kLookAhead) of the block
+    __shared__ uint32_t lmt[kTileMatches];   // the tile's compact match list from its conv point
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
     const uint64_t bstart = (uint64_t)b * L.B;
@@ -544,33 +550,65 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     const uint32_t t0 = k * kTile;
     if (t0 >= blen) return;
     const uint32_t t1 = min(blen, t0 + kTile);
-    {   // this tile's token and match counts: the next tile's offsets, or the block totals
-        const uint32_t tix = blockIdx.x;
-        const bool last = t1 == blen;
-        const uint32_t tk0 = tile_off[3 * tix], mk0 = tile_off[3 * tix + 1];
-        const uint32_t tk1 = last ? binfo[b].ntok : tile_off[3 * tix + 3];
-        const uint32_t mk1 = last ? binfo[b].nmatch : tile_off[3 * tix + 4];
-        if (tk1 - tk0 == t1 - t0 && mk1 == mk0 && ((uintptr_t)(in + bstart) & 3) == 0) {
-            emit_literal_tile(in + bstart, (const uint32_t *)(in + bstart), L.n - bstart, t0, t1 - t0, tk0,
-                              s_chars + (uint64_t)b * L.sstride[1], (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]));
-            return;
-        }
-    }
+    const uint32_t tix = blockIdx.x;
 
-    // this lane's 16 positions: one quarter of a chain word
-    const uint32_t s = t0 + tid * 16;
-    uint32_t bits = 0, mbs = 0;
+    // ---- round 1: independent loads ----
+    const bool last = t1 == blen;
+    const uint32_t tok0 = tile_off[3 * tix + 0], mi0 = tile_off[3 * tix + 1], g0 = tile_off[3 * tix + 2];
+    const uint32_t tk1 = last ? binfo[b].ntok : tile_off[3 * tix + 3];
+    const uint32_t mk1 = last ? binfo[b].nmatch : tile_off[3 * tix + 4];
+    const uint32_t cv = tconv[tix];
+    const uint32_t s = t0 + tid * 16;   // this lane's 16 positions: one quarter of a chain word
+    uint64_t cwv = 0, mbv = 0;
     if (s < t1) {
         const uint64_t wi = (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2);
-        bits = (uint32_t)(chain[wi] >> (16 * (tid & 3))) & 0xFFFFu;
-        mbs = (uint32_t)(mbits[wi] >> (16 * (tid & 3))) & 0xFFFFu;
+        cwv = chain[wi];
+        mbv = mbits[wi];
+    }
+    const uint8_t *d = in + bstart;
+    const bool al = (((uintptr_t)d) & 15) == 0;
+    uint32_t in4[4];
+    if (al && s + 16 <= blen) {
+        const uint4 v4 = *(const uint4 *)(d + s);
+        in4[0] = v4.x; in4[1] = v4.y; in4[2] = v4.z; in4[3] = v4.w;
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            uint32_t w = 0;
+            for (uint32_t j = 0; j < 4; j++)
+                if (s + 4 * q + j < blen) w |= (uint32_t)d[s + 4 * q + j] << (8 * j);
+            in4[q] = w;
+        }
+    }
+    uint32_t la = 0;   // look-ahead dword (match chars past the tile end)
+    const uint32_t xa = t0 + kTile + 4 * tid;
+    if (tid < kInW - kTile / 4 && xa < blen) {
+        if (al && xa + 4 <= blen) la = *(const uint32_t *)(d + xa);
+        else
+            for (uint32_t j = 0; j < 4 && xa + j < blen; j++) la |= (uint32_t)d[xa + j] << (8 * j);
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) lin[4 * tid + q] = in4[q];
+    if (tid < kInW - kTile / 4) lin[kTile / 4 + tid] = la;
+
+    if (tk1 - tok0 == t1 - t0 && mk1 == mi0) {   // no match token in the tile (uniform)
+        __syncthreads();
+        emit_literal_tile(lin, t1 - t0, tok0, s_chars + (uint64_t)b * L.sstride[1],
+                          (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]));
+        return;
+    }
+
+    uint32_t bits = 0, mbs = 0;
+    if (s < t1) {
+        bits = (uint32_t)(cwv >> (16 * (tid & 3))) & 0xFFFFu;
+        mbs = (uint32_t)(mbv >> (16 * (tid & 3))) & 0xFFFFu;
         const uint32_t valid = min(16u, t1 - s);
         if (valid < 16) bits &= (1u << valid) - 1;
     }
     // positions from the tile's conv point on (where the final chain joined the
     // speculative one) take their matches from the compact list, in order; the others
     // read m[] (first kResolveSpan positions, the stitch's walks, run-table tiles)
-    const uint32_t cv = tconv[blockIdx.x], crel = cv & 0xFFFFu;   // conv rel | dropped speculative matches << 16
+    const uint32_t crel = cv & 0xFFFFu;   // conv rel | dropped speculative matches << 16
     uint32_t post = 0;
     if (crel != kConvAll) {
         const uint32_t rel0 = s - t0;
@@ -578,11 +616,12 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     }
     const uint32_t rd = bits & mbs & ~post;   // chain positions whose m is in m[]
     const uint32_t rc = bits & mbs & post;    // chain matches in the compact list
-    uint32_t cbase = (uint32_t)__builtin_popcount(rc);
-    block_scan1(cbase, sh + 12);
+    uint32_t cbase = (uint32_t)__builtin_popcount(rc), ncomp;
+    block_scan1t(cbase, ncomp, sh + 12);       // (also publishes lin)
+
+    // ---- round 2: m rows and the compact list ----
     const uint32_t *mt = m + bstart + s;
     uint32_t mm[16];
-    uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0};
     if (rd && ((uintptr_t)mt & 15) == 0) {   // whole 64-B row as four 16-B loads
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
@@ -593,46 +632,39 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
 #pragma unroll
         for (uint32_t q = 0; q < 16; q++) mm[q] = ((rd >> q) & 1u) ? mt[q] : 0u;
     }
-    // the list starts at the tile's first speculative position: skip the matches the
-    // final chain dropped before the conv point
-    const uint32_t *mct = mtok + (uint64_t)blockIdx.x * kTileMatches + (cv >> 16) + cbase;
+    {   // the list starts at the tile's first speculative position: skip the matches the
+        // final chain dropped before the conv point
+        const uint32_t *mct = mtok + (uint64_t)tix * kTileMatches + (cv >> 16);
+        uint32_t cl[kTileMatches / 256];
+#pragma unroll
+        for (uint32_t u = 0; u < kTileMatches / 256; u++) cl[u] = tid + 256 * u < ncomp ? mct[tid + 256 * u] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kTileMatches / 256; u++) lmt[tid + 256 * u] = cl[u];
+    }
+    for (uint32_t w = tid; w < kFlagW; w += 256) lf[w] = 0;
+    for (uint32_t w = tid; w < kPW; w += 256) lp[w] = 0;
+    for (uint32_t w = tid; w < kGW; w += 256) lg[w] = 0;
+    for (uint32_t w = tid; w < kCharW; w += 256) lc[w] = 0;
+    __syncthreads();
+
+    uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0};
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
-        mm[q] = ((rd >> q) & 1u) ? mm[q] : ((rc >> q) & 1u) ? *mct++ : 0u;
+        const uint32_t ci = cbase + (uint32_t)__builtin_popcount(rc & ((1u << q) - 1u));
+        mm[q] = ((rd >> q) & 1u) ? mm[q] : ((rc >> q) & 1u) ? lmt[ci] : 0u;
         const uint32_t Lq = m_len(mm[q]);
         if (((bits >> q) & 1u) && Lq) { v[1]++; v[2] += (Lq >> 2) + 3; }
     }
     uint32_t tot[3];
     const uint32_t nm_lane = v[1];
     block_scan3(v, tot, sh);
-    const uint32_t tix = blockIdx.x;
-    const uint32_t tok0 = tile_off[3 * tix + 0], mi0 = tile_off[3 * tix + 1], g0 = tile_off[3 * tix + 2];
     const uint32_t tokA = tok0 + v[0], miA = mi0 + v[1];
     uint32_t goff = g0 + v[2];
     const uint32_t fw0 = tok0 >> 5, pw0 = (uint32_t)(((uint64_t)kPBits * mi0) >> 5), gw0 = g0 >> 5;
     const uint32_t cw0 = tok0 >> 2;   // chars staged on the global dword grid
-    for (uint32_t w = tid; w < kFlagW; w += 256) lf[w] = 0;
-    for (uint32_t w = tid; w < kPW; w += 256) lp[w] = 0;
-    for (uint32_t w = tid; w < kGW; w += 256) lg[w] = 0;
-    for (uint32_t w = tid; w < kCharW; w += 256) lc[w] = 0;
 
-    const uint8_t *d = in + bstart;
+    const uint8_t *lb = (const uint8_t *)lin;
     uint8_t *lcb = (uint8_t *)lc;
-    // the lane's 16 input bytes in one 16-B load: every literal char comes from here
-    uint32_t in4[4];
-    if (s + 16 <= blen && (((uintptr_t)(d + s)) & 15) == 0) {
-        const uint4 v4 = *(const uint4 *)(d + s);
-        in4[0] = v4.x; in4[1] = v4.y; in4[2] = v4.z; in4[3] = v4.w;
-    } else {
-#pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
-            uint32_t w = 0;
-            for (uint32_t j = 0; j < 4; j++)
-                if (s + 4 * q + j < t1) w |= (uint32_t)d[s + 4 * q + j] << (8 * j);
-            in4[q] = w;
-        }
-    }
-    __syncthreads();
     uint32_t fl = 0, nt_lane = 0;
     uint64_t pacc = 0;
     uint32_t np_lane = 0;
@@ -656,7 +688,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     for (uint32_t q = 0; q < 16; q++) {
         if ((bits >> q) & 1u) {
             const uint32_t Lm = m_len(mm[q]);
-            lcb[tokA + nt_lane - 4 * cw0] = Lm ? d[s + q + Lm] : (uint8_t)(in4[q >> 2] >> (8 * (q & 3)));
+            lcb[tokA + nt_lane - 4 * cw0] = Lm ? lb[s - t0 + q + Lm] : (uint8_t)(in4[q >> 2] >> (8 * (q & 3)));
             if (Lm == 0) {
                 fl |= 1u << nt_lane;
             } else {
