@@ -22,7 +22,7 @@
 //   k_scan_blocks  record offsets across the shard (+ capacity check)
 //   k_zero_edges   zero the words the encoder ORs into (the two edge words of every
 //                  chunk; every other output byte is stored whole by k_encode or k_headers)
-//   k_encode       each lane packs its 32 codes into whole words (LDS atomics only
+//   k_encode       each lane packs its 64 codes into whole words (LDS atomics only
 //                  for the two words it shares with neighbours); the chunk's words
 //                  are stored at the record's (unaligned) byte offset: interior
 //                  words plain, chunk-edge words atomicOr
@@ -46,22 +46,35 @@ __device__ inline void chunk_of(const Layout &L, uint32_t r, uint32_t &s, uint32
 }
 
 // ---------------------------------------------------------------------------
-__device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32_t i1, uint32_t *out32 /*8 words*/) {
-    // loads the (up to) 32 symbols [i0, i1) as two 16-B loads (i0 is a multiple of 32
-    // and stream strides are multiples of 16; the buffers carry slack past the end),
+// a chunk's workgroup: kEncT lanes of kSymL consecutive symbols (64 B per lane in flight:
+// two waves per 8 KiB chunk, so a CU holds 16 chunks' loads at once)
+constexpr uint32_t kEncT = 128;
+constexpr uint32_t kSymL = kChunk / kEncT;   // 64
+constexpr uint32_t kSymW = kSymL / 4;        // 16 words
+static_assert(kSymL % 16 == 0, "whole 16-B loads");
+
+__device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32_t i1, uint32_t *out32 /*kSymW words*/) {
+    // loads the (up to) kSymL symbols [i0, i1) as 16-B loads, all in flight together (i0 is
+    // a multiple of kSymL and stream strides are multiples of 16; a read past a block's
+    // stream lands in the next block's stride or the 64 B of slack at the buffer end),
     // bytes past i1 zeroed
     const uint32_t n = i1 > i0 ? i1 - i0 : 0;
     if (n == 0) {
 #pragma unroll
-        for (uint32_t q = 0; q < 8; q++) out32[q] = 0;
+        for (uint32_t q = 0; q < kSymW; q++) out32[q] = 0;
         return 0;
     }
-    const uint4 a = ((const uint4 *)(w4 + (i0 >> 2)))[0], b = ((const uint4 *)(w4 + (i0 >> 2)))[1];
-    out32[0] = a.x; out32[1] = a.y; out32[2] = a.z; out32[3] = a.w;
-    out32[4] = b.x; out32[5] = b.y; out32[6] = b.z; out32[7] = b.w;
-    if (n < 32)
+    const uint4 *p = (const uint4 *)(w4 + (i0 >> 2));
+    uint4 v[kSymW / 4];
 #pragma unroll
-        for (uint32_t q = 0; q < 8; q++) {
+    for (uint32_t q = 0; q < kSymW / 4; q++) v[q] = p[q];
+#pragma unroll
+    for (uint32_t q = 0; q < kSymW / 4; q++) {
+        out32[4 * q] = v[q].x; out32[4 * q + 1] = v[q].y; out32[4 * q + 2] = v[q].z; out32[4 * q + 3] = v[q].w;
+    }
+    if (n < kSymL)
+#pragma unroll
+        for (uint32_t q = 0; q < kSymW; q++) {
             const uint32_t lo = 4 * q;
             out32[q] = lo >= n ? 0u : (n - lo >= 4 ? out32[q] : out32[q] & ((1u << (8 * (n - lo))) - 1u));
         }
@@ -73,11 +86,12 @@ __device__ inline const uint8_t *stream_base(const Layout &L, uint32_t s, uint32
     return (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
 }
 
-__global__ __launch_bounds__(256) void k_hist(Layout L, const BlockInfo *__restrict__ binfo,
-                                              const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
-                                              const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
-                                              uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[4][256];
+__global__ __launch_bounds__(kEncT) void k_hist(Layout L, const BlockInfo *__restrict__ binfo,
+                                                const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
+                                                const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
+                                                uint32_t *__restrict__ hist) {
+    constexpr uint32_t kW = kEncT / 64;
+    __shared__ uint32_t h[kW][256];
     const uint32_t tid = threadIdx.x, wv = tid >> 6;
     const uint32_t b = blockIdx.x / L.cpb_total;
     uint32_t s, c;
@@ -87,12 +101,12 @@ __global__ __launch_bounds__(256) void k_hist(Layout L, const BlockInfo *__restr
     const uint32_t len = bi.slen[s], c0 = c * kChunk;
     if (c0 >= len) return;
     const uint32_t c1 = min(len, c0 + kChunk);
-    for (uint32_t x = tid; x < 1024; x += 256) (&h[0][0])[x] = 0;
-    __syncthreads();
-    // each lane counts a strip of 32 consecutive symbols, runs of one byte value first
-    const uint32_t i0 = c0 + 32 * tid, i1 = min(c1, i0 + 32);
-    uint32_t sym[8];
+    // each lane counts a strip of kSymL consecutive symbols, runs of one byte value first
+    const uint32_t i0 = c0 + kSymL * tid, i1 = min(c1, i0 + kSymL);
+    uint32_t sym[kSymW];
     const uint32_t n = chunk_symbols((const uint32_t *)stream_base(L, s, b, s0, s1, s2, s3), i0, i1, sym);
+    for (uint32_t x = tid; x < kW * 256; x += kEncT) (&h[0][0])[x] = 0;
+    __syncthreads();
     uint32_t cur = sym[0] & 0xFF, run = 0;
     for (uint32_t q = 0; q < n; q++) {
         const uint32_t v = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
@@ -105,7 +119,12 @@ __global__ __launch_bounds__(256) void k_hist(Layout L, const BlockInfo *__restr
     }
     if (run) atomicAdd(&h[wv][cur], run);
     __syncthreads();
-    hist[(uint64_t)blockIdx.x * 256 + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    for (uint32_t x = tid; x < 256; x += kEncT) {
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kW; w++) t += h[w][x];
+        hist[(uint64_t)blockIdx.x * 256 + x] = t;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -327,68 +346,82 @@ __global__ __launch_bounds__(256) void k_zero_edges(Layout L, const BlockInfo *_
     }
 }
 
-constexpr uint32_t kEncWords = kChunk + 2;  // codes <= 32 bits
+// staging words: the whole chunk at <= 8 bits per symbol (one pass; random data's chars
+// are exactly 8); longer codes (<= 32 bits) go through several windows of this size
+constexpr uint32_t kEncWords = kChunk / 4 + 2;
 
-__global__ __launch_bounds__(256) void k_encode(Layout L, const BlockInfo *__restrict__ binfo,
-                                                const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
-                                                const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
-                                                const uint32_t *__restrict__ ctab, const uint8_t *__restrict__ ltab,
-                                                const uint32_t *__restrict__ chunk_off,
-                                                const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
-                                                const uint32_t *__restrict__ err) {
+__global__ __launch_bounds__(kEncT) void k_encode(Layout L, const BlockInfo *__restrict__ binfo,
+                                                 const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
+                                                 const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
+                                                 const uint32_t *__restrict__ ctab, const uint8_t *__restrict__ ltab,
+                                                 const uint32_t *__restrict__ chunk_off,
+                                                 const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
+                                                 const uint32_t *__restrict__ err) {
+    constexpr uint32_t kW = kEncT / 64;
     __shared__ uint32_t ct[256], lt[256];
     __shared__ uint32_t ws[kEncWords];
-    __shared__ uint32_t red[4];
-    if (*err) return;
+    __shared__ uint32_t red[kW];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / L.cpb_total, r = blockIdx.x % L.cpb_total;
     uint32_t s, c;
     chunk_of(L, r, s, c);
+    // loads in two rounds: error word + block info, then everything else at once
+    const uint32_t errv = *err;
     const BlockInfo &bi = binfo[b];
     const uint32_t len = bi.slen[s], c0 = c * kChunk;
-    if (!stream_active(bi, s) || c0 >= len) return;
+    if (errv || !stream_active(bi, s) || c0 >= len) return;
     const uint32_t c1 = min(len, c0 + kChunk);
     const uint32_t hb = (b * kStreams + s) * 256;
-    ct[tid] = ctab[hb + tid];
-    lt[tid] = ltab[hb + tid];
+    uint32_t ctv[256 / kEncT], ltv[256 / kEncT];
+#pragma unroll
+    for (uint32_t u = 0; u < 256 / kEncT; u++) { ctv[u] = ctab[hb + tid + kEncT * u]; ltv[u] = ltab[hb + tid + kEncT * u]; }
+    const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
+    const uint32_t i0 = c0 + kSymL * tid, i1 = min(c1, i0 + kSymL);
+    uint32_t sym[kSymW];
+    const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
+    const uint64_t obyte = blk_off[b] + bi.words_rel[s];
+    const uint32_t coff = chunk_off[(uint64_t)b * L.cpb_total + r];
+    bool all8 = true;
+#pragma unroll
+    for (uint32_t u = 0; u < 256 / kEncT; u++) {
+        ct[tid + kEncT * u] = ctv[u];
+        lt[tid + kEncT * u] = ltv[u];
+        all8 = all8 && ltv[u] == 8;
+    }
     // all 256 symbols with 8-bit codes (the chars of random data): the code stream is a
     // byte substitution at a byte-aligned offset
-    const bool byte8 = __syncthreads_and(lt[tid] == 8) != 0;
-    const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
-    const uint32_t i0 = c0 + 32 * tid, i1 = min(c1, i0 + 32);
-    uint32_t sym[8];
-    const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
+    const bool byte8 = __syncthreads_and(all8) != 0;
     if (byte8) {
-        const uint64_t g0 = 8 * (blk_off[b] + bi.words_rel[s]) + chunk_off[(uint64_t)b * L.cpb_total + r];
+        const uint64_t g0 = 8 * obyte + coff;
         const uint32_t sh0 = (uint32_t)(g0 & 31), nw = (sh0 + 8 * (c1 - c0) + 31) >> 5;
-        for (uint32_t x = tid; x < nw; x += 256) ws[x] = 0;
-        uint32_t v[9];
+        for (uint32_t x = tid; x < nw; x += kEncT) ws[x] = 0;
+        uint32_t v[kSymW + 1];
 #pragma unroll
-        for (uint32_t q = 0; q < 8; q++) {
+        for (uint32_t q = 0; q < kSymW; q++) {
             const uint32_t w = sym[q];
             v[q] = ct[w & 0xFF] | (ct[(w >> 8) & 0xFF] << 8) | (ct[(w >> 16) & 0xFF] << 16) | (ct[w >> 24] << 24);
             if (4 * q >= n) v[q] = 0;
             else if (n - 4 * q < 4) v[q] &= (1u << (8 * (n - 4 * q))) - 1u;
         }
-        // this lane's bytes start at staging byte sh0/8 + 32 tid: shift into 9 words,
-        // the first and last shared with the neighbouring lanes
-        const uint32_t bo = (sh0 >> 3) + 32 * tid, sb = 8 * (bo & 3), w0 = bo >> 2;
-        v[8] = 0;
+        // this lane's bytes start at staging byte sh0/8 + kSymL tid: shift into kSymW + 1
+        // words, the first and last two shared with the neighbouring lanes
+        const uint32_t bo = (sh0 >> 3) + kSymL * tid, sb = 8 * (bo & 3), w0 = bo >> 2;
+        v[kSymW] = 0;
         __syncthreads();
         if (n) {
             uint32_t prev = 0;
 #pragma unroll
-            for (uint32_t q = 0; q < 9; q++) {
+            for (uint32_t q = 0; q <= kSymW; q++) {
                 const uint32_t cur = v[q];
                 const uint32_t o = sb ? (cur << sb) | (prev >> (32 - sb)) : cur;
                 prev = cur;
-                if (q == 0 || q >= 7) { if (o) atomicOr(&ws[w0 + q], o); }
+                if (q == 0 || q >= kSymW - 1) { if (o) atomicOr(&ws[w0 + q], o); }
                 else ws[w0 + q] = o;
             }
         }
         __syncthreads();
         uint32_t *o32 = (uint32_t *)out + (g0 >> 5);
-        for (uint32_t x = tid; x < nw; x += 256) {
+        for (uint32_t x = tid; x < nw; x += kEncT) {
             const uint32_t val = ws[x];
             if (x == 0 || x == nw - 1) { if (val) atomicOr(&o32[x], val); }
             else o32[x] = val;
@@ -402,42 +435,51 @@ __global__ __launch_bounds__(256) void k_encode(Layout L, const BlockInfo *__res
     if (lane == 63) red[wv] = inc;
     __syncthreads();
     uint32_t pre = 0, ctot = 0;
-    for (uint32_t q = 0; q < 4; q++) {
+    for (uint32_t q = 0; q < kW; q++) {
         if (q < wv) pre += red[q];
         ctot += red[q];
     }
     const uint32_t tb = pre + inc - nb;
-    const uint64_t obyte = blk_off[b] + bi.words_rel[s];
-    const uint64_t g0 = 8 * obyte + chunk_off[(uint64_t)b * L.cpb_total + r];
+    const uint64_t g0 = 8 * obyte + coff;
     const uint64_t gw = g0 >> 5;
     const uint32_t sh0 = (uint32_t)(g0 & 31);
     const uint32_t nw = (sh0 + ctot + 31) >> 5;
-    for (uint32_t x = tid; x < nw; x += 256) ws[x] = 0;
-    __syncthreads();
     // this lane's codes cover bits [p0, p1) of the staging words; whole words inside
-    // that range are this lane's alone (plain LDS stores), the two end words are shared
+    // that range are this lane's alone (plain LDS stores), the two end words are shared.
+    // Windows of kEncWords words: a lane writes the words of its range inside the window.
     const uint32_t p0 = sh0 + tb, p1 = p0 + nb;
-    uint32_t wi = p0 >> 5, ap = p0 & 31;
-    uint64_t acc = 0;
-    for (uint32_t q = 0; q < n; q++) {
-        const uint32_t sy = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
-        acc |= (uint64_t)ct[sy] << ap;
-        ap += lt[sy];
-        if (ap >= 32) {
-            if (32 * wi >= p0 && 32 * wi + 32 <= p1) ws[wi] = (uint32_t)acc;
-            else atomicOr(&ws[wi], (uint32_t)acc);
-            acc >>= 32;
-            ap -= 32;
-            wi++;
-        }
-    }
-    if (ap) atomicOr(&ws[wi], (uint32_t)acc);
-    __syncthreads();
     uint32_t *o32 = (uint32_t *)out + gw;
-    for (uint32_t x = tid; x < nw; x += 256) {
-        const uint32_t v = ws[x];
-        if (x == 0 || x == nw - 1) { if (v) atomicOr(&o32[x], v); }
-        else o32[x] = v;
+    for (uint32_t wb = 0; wb < nw; wb += kEncWords) {
+        const uint32_t we = min(nw, wb + kEncWords);
+        for (uint32_t x = tid; x < we - wb; x += kEncT) ws[x] = 0;
+        __syncthreads();
+        if (nb && (p0 >> 5) < we && ((p1 - 1) >> 5) >= wb) {
+            uint32_t wi = p0 >> 5, ap = p0 & 31;
+            uint64_t acc = 0;
+            for (uint32_t q = 0; q < n; q++) {
+                const uint32_t sy = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
+                acc |= (uint64_t)ct[sy] << ap;
+                ap += lt[sy];
+                if (ap >= 32) {
+                    if (wi >= wb && wi < we) {
+                        if (32 * wi >= p0 && 32 * wi + 32 <= p1) ws[wi - wb] = (uint32_t)acc;
+                        else atomicOr(&ws[wi - wb], (uint32_t)acc);
+                    }
+                    acc >>= 32;
+                    ap -= 32;
+                    wi++;
+                    if (wi >= we) break;
+                }
+            }
+            if (ap && wi >= wb && wi < we) atomicOr(&ws[wi - wb], (uint32_t)acc);
+        }
+        __syncthreads();
+        for (uint32_t x = wb + tid; x < we; x += kEncT) {
+            const uint32_t v = ws[x - wb];
+            if (x == 0 || x == nw - 1) { if (v) atomicOr(&o32[x], v); }
+            else o32[x] = v;
+        }
+        __syncthreads();
     }
 }
 
@@ -479,7 +521,7 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
                     uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
                     hipEvent_t *ev) {
     const uint32_t nchunks = L.nblocks * L.cpb_total;
-    hipLaunchKernelGGL(k_hist, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, hist);
+    hipLaunchKernelGGL(k_hist, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, hist);
     if (ev) (void)hipEventRecord(ev[0], st);
     hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(64), 0, st, L, hist, binfo, ctab, ltab, hhdr,
                        chunk_off, err);
@@ -491,7 +533,7 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
     hipLaunchKernelGGL(k_zero_edges, dim3((nchunks + 255) / 256), dim3(256), 0, st, L, binfo, chunk_off, blk_off, out,
                        err);
     if (ev) (void)hipEventRecord(ev[4], st);
-    hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(256), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, chunk_off,
+    hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, chunk_off,
                        blk_off, out, err);
     if (ev) (void)hipEventRecord(ev[5], st);
     hipLaunchKernelGGL(k_headers, dim3(L.nblocks), dim3(64), 0, st, binfo, s0, L.sstride[0], hhdr, blk_off, out, err);

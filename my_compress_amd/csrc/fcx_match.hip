@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
                                               uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg) {
-    __shared__ uint32_t sdw[kTileBytes / 4 + 4];           // byte image of the window
+    __shared__ __attribute__((aligned(16))) uint32_t sdw[kTileBytes / 4 + 4];   // byte image of the window
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
     // search, [step (u16 x 4096) | parse scratch] after it
     __shared__ __attribute__((aligned(16))) uint32_t region[kRegionWords];
@@ -393,15 +393,24 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
     // ---- 1. stage bytes (zero padded) ----
     const uint8_t *src = d + w0;
-    if ((((uintptr_t)src) & 3) == 0) {
-        const uint32_t *src4 = (const uint32_t *)src;
-        const uint32_t nfull = nload >> 2;
-        for (uint32_t x = tid; x < kTileBytes / 4 + 4; x += kMT) {
-            uint32_t v = 0;
-            if (x < nfull) v = src4[x];
-            else if (x == nfull)
-                for (uint32_t q = 0; q < (nload & 3); q++) v |= (uint32_t)src[4 * x + q] << (8 * q);
-            sdw[x] = v;
+    static_assert((kTileBytes / 4 + 4) % 4 == 0 && (kTileBytes / 4 + 4) / 4 <= kMT, "one 16-B load per lane");
+    if ((((uintptr_t)src) & 15) == 0) {
+        // one 16-B load per lane, all in flight at once
+        if (tid < (kTileBytes / 4 + 4) / 4) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (16 * tid + 16 <= nload) v = ((const uint4 *)src)[tid];
+            else if (16 * tid < nload) {
+                uint32_t w[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    w[q] = 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++)
+                        if (16 * tid + 4 * q + j < nload) w[q] |= (uint32_t)src[16 * tid + 4 * q + j] << (8 * j);
+                }
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            ((uint4 *)sdw)[tid] = v;
         }
     } else {
         for (uint32_t x = tid; x < kTileBytes / 4 + 4; x += kMT) {

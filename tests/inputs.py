@@ -115,6 +115,12 @@ def golden_specs():
         {"type": "gen", "kind": "text", "seed": 21, "n": 100000},
         {"type": "gen", "kind": "zeros", "seed": 0, "n": 50000},
         {"type": "gen", "kind": "text", "seed": 22, "n": 100000}]})
+    # a chars stream whose random stretch has Huffman codes far above 8 bits (text sets
+    # the frequencies): chunks there take several encode staging windows
+    S.append({"name": "text_rand_text_longcodes", "type": "concat", "block": MiB, "parts": [
+        {"type": "gen", "kind": "text", "seed": 23, "n": 600000},
+        {"type": "gen", "kind": "rand", "seed": 24, "n": 40000},
+        {"type": "gen", "kind": "text", "seed": 25, "n": 300000}]})
     S.append({"name": "text_plus_partial", "type": "concat", "block": 262144, "parts": [
         {"type": "gen", "kind": "text", "seed": 5, "n": MiB + 12345}]})
     # decoder quirks (my_compress.cpp:2255-2393): an all-literal block whose flag bytes
