@@ -731,6 +731,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     Gs[tid + 1] = X;
     if (tid == 0) Gs[0] = t0;
     __syncthreads();
+    if (dbg & 512u) return;   // timing: + sub-segment walks
     // Jacobi rounds.  A segment is active when its entry lies inside it; the next
     // entry of segment k + 1 is the exit of the nearest active segment <= k (a
     // block-wide running max of active indices), so a long token passes over any
@@ -766,6 +767,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         __syncthreads();
         if (!s_chg[r & 1]) break;
     }
+    if (dbg & 256u) return;   // timing: + Jacobi rounds
     // counts of this lane's chain positions, prefix over lanes
     uint32_t cnt[3] = {(uint32_t)__builtin_popcount(T), 0, 0};
     for (uint32_t bits = T; bits; bits &= bits - 1) {

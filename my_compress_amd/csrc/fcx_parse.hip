@@ -80,27 +80,6 @@ __device__ void load_window(uint32_t *dw, const uint8_t *d, uint32_t dbase, uint
     }
 }
 
-// set bit `setb` (if != ~0) and clear bits [lo, hi) of an LDS bitmap, lane-parallel
-__device__ inline void bm_apply(uint64_t *bm, uint32_t setb, uint32_t lo, uint32_t hi) {
-    const uint32_t lane = lane_id();
-    uint32_t first = 0xFFFFFFFFu, last = 0;
-    if (setb != 0xFFFFFFFFu) { first = setb; last = setb; }
-    if (hi > lo) { first = min(first, lo); last = max(last, hi - 1); }
-    if (first == 0xFFFFFFFFu) return;
-    const uint32_t wlo = first >> 6, whi = last >> 6;
-    for (uint32_t w = wlo + lane; w <= whi; w += 64) {
-        uint64_t v = bm[w];
-        const uint32_t a = max(lo, w * 64), z = min(hi, w * 64 + 64);
-        if (z > a) {
-            const uint32_t n = z - a;
-            const uint64_t msk = (n == 64 ? ~0ull : ((1ull << n) - 1)) << (a - w * 64);
-            v &= ~msk;
-        }
-        if (setb != 0xFFFFFFFFu && (setb >> 6) == w) v |= 1ull << (setb & 63);
-        bm[w] = v;
-    }
-}
-
 struct Cnt3 {
     uint32_t tok, mat, gb;
     __device__ void add(uint32_t L) {
@@ -272,6 +251,20 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     (void)conv;
 }
 
+// one tile's m rows (16 x 16 B per lane), mbits word and chain word (lane < nw), all in
+// flight together
+__device__ inline void fetch_tile(const uint32_t *mt, const uint64_t *mb, const uint64_t *cw, uint32_t nt, uint32_t nw,
+                                  uint4 *v, uint64_t &mbw, uint64_t &cwv) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t q = 0; q < kTile / 256; q++) {
+        const uint32_t x = 4 * (lane + 64 * q);
+        v[q] = x + 4 <= nt ? ((const uint4 *)mt)[lane + 64 * q] : make_uint4(0, 0, 0, 0);
+    }
+    mbw = lane < nw ? mb[lane] : 0ull;
+    cwv = lane < nw ? cw[lane] : 0ull;
+}
+
 __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                                const uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain, const uint64_t *__restrict__ chain_pfx,
                                                const uint32_t *__restrict__ tinfo, const uint64_t *__restrict__ fp,
@@ -293,6 +286,9 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
     const uint32_t ntiles = (blen + kTile - 1) / kTile;
     uint32_t e = 0, dbase = 0xFFFFFFFFu, nlazy = 0, lazy_tiles = 0;
     Cnt3 run{0, 0, 0};
+    uint4 pv[kTile / 256];   // prefetched rows / mbits / chain word of tile pk
+    uint64_t pmb = 0, pcw = 0;
+    uint32_t pk = 0xFFFFFFFFu;
 
     for (uint32_t k = 0; k < ntiles; k++) {
         const uint32_t t0 = k * kTile, t1 = min(blen, t0 + kTile);
@@ -345,22 +341,21 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         }
         // ---- slow path ----
         lazy_tiles += lazy ? 1 : 0;
-        mbL[lane] = lane < nw ? mb[lane] : 0ull;   // one mbits word per lane (64 words per tile)
-        __syncthreads();
         const uint32_t nt = t1 - t0;
-        if ((((uintptr_t)mt) & 15) == 0) {   // 16 independent 16-B loads per lane, then masked LDS stores
-            uint4 v[kTile / 256];
+        const bool vec = (((uintptr_t)mt) & 15) == 0;
+        if (vec) {
+            // this tile's rows, mbits and chain words: prefetched during the previous tile's
+            // walk (run-table tiles, whose entries rarely match k_resolve's), else loaded now
+            if (pk != k) fetch_tile(mt, mb, cw, nt, nw, pv, pmb, pcw);
+            mbL[lane] = pmb;
+            bmL[lane] = pcw;
 #pragma unroll
             for (uint32_t q = 0; q < kTile / 256; q++) {
                 const uint32_t x = 4 * (lane + 64 * q);
-                v[q] = x + 4 <= nt ? ((const uint4 *)mt)[lane + 64 * q] : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < kTile / 256; q++) {
-                const uint32_t x = 4 * (lane + 64 * q);
+                const uint64_t mw = __shfl(pmb, (lane >> 4) + 4 * q, 64);   // mbits word of x
                 if (x >= nt) continue;
-                const uint32_t mbw = (uint32_t)(mbL[x >> 6] >> (x & 63)) & 0xFu;
-                const uint32_t vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+                const uint32_t mbw = (uint32_t)(mw >> (x & 63)) & 0xFu;
+                const uint32_t vv[4] = {pv[q].x, pv[q].y, pv[q].z, pv[q].w};
 #pragma unroll
                 for (uint32_t u = 0; u < 4; u++)
                     if (x + u < nt)
@@ -368,15 +363,25 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                                                                                       : kUnknown)
                                                       : 0u;
             }
+            pk = 0xFFFFFFFFu;
+            if (k + 1 < ntiles && j + 1 < 64 && (sti[j + 1][0] & kTileMFull)) {
+                const uint32_t u0 = t1, u1 = min(blen, u0 + kTile);
+                fetch_tile(m + bstart + u0, mb + kTile / 64, cw + kTile / 64, u1 - u0, (u1 - u0 + 63) / 64, pv, pmb, pcw);
+                pk = k + 1;
+            }
         } else {
+            mbL[lane] = lane < nw ? mb[lane] : 0ull;   // one mbits word per lane (64 words per tile)
+            __syncthreads();
             for (uint32_t x = lane; x < nt; x += 64)   // m only where the position's mbits bit is set
                 mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? (mfull || x < kResolveSpan ? mt[x] : kUnknown) : 0u;
+            for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
         }
-        for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
         __syncthreads();
-        if (e > t0) bm_apply(bmL, 0xFFFFFFFFu, 0, e - t0);
-        __syncthreads();
-        uint32_t t = e, exitv, convrec = kConvAll;
+        // the walk is wave-uniform and reads only LDS written above: no barrier per token.
+        // Lane w keeps the walked chain bits of word w; the speculative bits stay from the
+        // stop point (conv point, or the tile end) on.
+        uint64_t nwb = 0;
+        uint32_t t = e, exitv, convrec = kConvAll, stop;
         Cnt3 walked{0, 0, 0};
         for (;;) {
             const uint32_t rel = t - t0;
@@ -389,6 +394,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 walked.mat += tot.mat - drop.mat;
                 walked.gb += tot.gb - drop.gb;
                 exitv = sti[j][1];
+                stop = rel;
                 break;
             }
             uint32_t mm = mL[rel];
@@ -405,14 +411,15 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 if (lane == 0) m[bstart + t] = mm;
             }
             walked.add(m_len(mm));
-            const uint32_t nt = t + m_len(mm) + 1;
-            bm_apply(bmL, rel, rel + 1, min(nt, t1) - t0);
-            __syncthreads();
-            t = nt;
-            if (t >= t1) { exitv = t; break; }
+            if (lane == (rel >> 6)) nwb |= 1ull << (rel & 63);
+            t += m_len(mm) + 1;
+            if (t >= t1) { exitv = t; stop = nt; break; }
         }
-        __syncthreads();
-        for (uint32_t w = lane; w < nw; w += 64) cw[w] = bmL[w];
+        if (lane < nw) {
+            const uint32_t lo = 64 * lane;
+            const uint64_t keep = stop <= lo ? ~0ull : stop >= lo + 64 ? 0ull : ~0ull << (stop - lo);
+            cw[lane] = (bmL[lane] & keep) | nwb;
+        }
         if (lane == 0) tconv[tix] = convrec;
         __syncthreads();
         run.tok += walked.tok; run.mat += walked.mat; run.gb += walked.gb;
