@@ -36,6 +36,17 @@ __host__ __device__ inline uint32_t m_dist(uint32_t m) { return m & 0x7FFu; }
 
 constexpr uint32_t kTileLazy = 1u;   // tile_flags: spec parse unavailable, stitch walks it
 constexpr uint32_t kTileMFull = 2u;  // tile_flags: m[] holds every match / unknown of the tile (run table ran)
+constexpr uint32_t kTileUniform = 4u;  // tile_flags: the tile's window is one byte value; m is m_uniform, no m[] rows
+
+// m of block position i when the whole window [i - 2047, i + 258) and the block start
+// side of it hold one byte value: every window position matches up to the cap, and the
+// leftmost one wins (distance min(i, 2047)); literal at the block start and in the
+// last three bytes (my_compress.cpp:1446-1514, 1675-1714)
+__host__ __device__ inline uint32_t m_uniform(uint32_t i, uint32_t blen) {
+    if (i == 0 || blen - i < 4) return 0u;
+    const uint32_t L = (blen - i < kMaxL ? blen - i : kMaxL) - 1;
+    return m_pack(L, i < kWin ? i : kWin);
+}
 constexpr uint32_t kResolveSpan = 256;           // k_resolve's walk limit; m[] rows always kept below it
 constexpr uint32_t kTileMatches = kTile / 4;     // compact match list slots per tile (a match covers >= 4)
 constexpr uint32_t kConvAll = 0xFFFFu;           // tile conv record: k_emit takes every m from m[]

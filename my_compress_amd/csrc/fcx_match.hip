@@ -359,6 +359,42 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
     }
 }
 
+// ---- uniform tiles (one byte value over the whole image): m = m_uniform ----
+// step and mbits of the tile's positions (mbw: the block's mbits words)
+__device__ inline void uniform_step(uint16_t *step, uint64_t *mbw, uint32_t *s_match, uint32_t t0, uint32_t t1,
+                                          uint32_t blen) {
+    const uint32_t tid = threadIdx.x;
+    bool any = false;
+#pragma unroll
+    for (uint32_t r = 0; r < kQPL; r++) {
+        const uint32_t rel = tid + kMT * r, i = t0 + rel;
+        const uint32_t mu = i < t1 ? m_uniform(i, blen) : 0u;
+        step[rel] = (uint16_t)(mu ? m_len(mu) + 1 : 1);
+        any = any || mu != 0;
+        const uint64_t mb = __ballot(mu != 0);
+        if ((tid & 63) == 0 && i < t1) mbw[i >> 6] = mb;
+    }
+    if (any) *s_match = 1;
+    __syncthreads();
+}
+
+// the speculative chain from t0 follows from m_uniform: every lane walks it (<= 17
+// tokens to its sub-segment [s, se)); returns the lane's chain bits, the lane holding
+// the tile's last position writes the exit to Gs[nsub]
+__device__ inline uint32_t uniform_chain(uint32_t *Gs, uint32_t s, uint32_t se, uint32_t t0, uint32_t t1,
+                                               uint32_t blen) {
+    auto ustep = [&](uint32_t p) -> uint32_t {
+        const uint32_t mu = m_uniform(p, blen);
+        return mu ? m_len(mu) + 1 : 1u;
+    };
+    uint32_t T = 0, p = t0;
+    while (p < s) p += ustep(p);
+    while (p < se) { T |= 1u << (p - s); p += ustep(p); }
+    if (s < t1 && se == t1) Gs[(t1 - t0 + kSeg - 1) / kSeg] = p;
+    __syncthreads();
+    return T;
+}
+
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
@@ -468,6 +504,9 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     __syncthreads();
     const bool rmode = (s_nruns <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
+    // one byte value over the whole image (zeros): m is m_uniform, no search, no m[] rows.
+    // Re-read from LDS where used (nothing held in registers across the search)
+    auto uniform_tile = [&]() -> bool { return s_nruns == 1 && !(dbg & 12u); };
     if (dbg & 16u) return;   // timing: staging + run count only
 
     // this lane's 12 consecutive window positions 12 tid .. 12 tid + 11 take their keys from
@@ -481,7 +520,9 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         return key_mix(__builtin_amdgcn_alignbyte(kw[(r >> 2) + 1], kw[r >> 2], r & 3) & 0xFFFFFFu);
     };
 
-    if (rmode) {
+    if (uniform_tile()) {
+        uniform_step(step, mbits + (uint64_t)b * L.wpb, &s_match, t0, t1, blen);
+    } else if (rmode) {
         for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
         if (tid == 0) s_unknown = 1;
         __syncthreads();
@@ -719,55 +760,59 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     uint32_t *Vs = Xs + kMT;
     const uint32_t s = t0 + tid * kSeg;
     const uint32_t se = min(s + kSeg, t1);
-    uint32_t V = 0, X = s;
     uint32_t T = 0;
-    uint32_t *Ys = Vs;   // exits of a Jacobi round (Vs is free until the counts below)
-    if (s < t1) {
-        uint32_t t = s;
-        while (t < se) { V |= 1u << (t - s); t += step[t - t0]; }
-        X = t;
-    }
-    Xs[tid] = X;
-    Gs[tid + 1] = X;
-    if (tid == 0) Gs[0] = t0;
-    __syncthreads();
-    if (dbg & 512u) return;   // timing: + sub-segment walks
-    // Jacobi rounds.  A segment is active when its entry lies inside it; the next
-    // entry of segment k + 1 is the exit of the nearest active segment <= k (a
-    // block-wide running max of active indices), so a long token passes over any
-    // number of segments in one round.
-    for (uint32_t r = 0;; r++) {
-        const uint32_t e = Gs[tid];
-        uint32_t ex;
-        bool act = false;
-        if (s >= t1 || e >= se) {
-            ex = e; T = 0;
-        } else if ((V >> (e - s)) & 1u) {
-            act = true; ex = X; T = V & (~0u << (e - s));
-        } else {
-            act = true; T = 0;
-            uint32_t t = e;
-            while (t < se && !((V >> (t - s)) & 1u)) { T |= 1u << (t - s); t += step[t - t0]; }
-            if (t < se) { ex = X; T |= V & (~0u << (t - s)); }
-            else ex = t;
+    if (uniform_tile()) {
+        T = uniform_chain(Gs, s, se, t0, t1, blen);
+    } else {
+        uint32_t V = 0, X = s;
+        uint32_t *Ys = Vs;   // exits of a Jacobi round (Vs is free until the counts below)
+        if (s < t1) {
+            uint32_t t = s;
+            while (t < se) { V |= 1u << (t - s); t += step[t - t0]; }
+            X = t;
         }
-        Ys[tid] = ex;
-        // nearest active segment <= tid: highest set bit of the wave's ballot at or
-        // below this lane, else the last active segment of an earlier wave
-        const uint64_t am = __ballot(act);
-        const uint32_t lane = tid & 63;
-        if (lane == 0) s_red[tid >> 6] = am ? (tid & ~63u) + 64 - (uint32_t)__clzll(am) : 0u;
+        Xs[tid] = X;
+        Gs[tid + 1] = X;
+        if (tid == 0) Gs[0] = t0;
         __syncthreads();
-        const uint64_t le = am & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-        uint32_t li = le ? (tid & ~63u) + 64 - (uint32_t)__clzll(le) : 0u;
-        for (int w = (int)(tid >> 6) - 1; w >= 0 && !li; w--) li = s_red[w];
-        const uint32_t ne = li ? Ys[li - 1] : Gs[tid + 1];
-        if (ne != Gs[tid + 1]) { Gs[tid + 1] = ne; s_chg[r & 1] = 1; }
-        if (tid == 0) s_chg[(r + 1) & 1] = 0;
-        __syncthreads();
-        if (!s_chg[r & 1]) break;
+        if (dbg & 512u) return;   // timing: + sub-segment walks
+        // Jacobi rounds.  A segment is active when its entry lies inside it; the next
+        // entry of segment k + 1 is the exit of the nearest active segment <= k (a
+        // block-wide running max of active indices), so a long token passes over any
+        // number of segments in one round.
+        for (uint32_t r = 0;; r++) {
+            const uint32_t e = Gs[tid];
+            uint32_t ex;
+            bool act = false;
+            if (s >= t1 || e >= se) {
+                ex = e; T = 0;
+            } else if ((V >> (e - s)) & 1u) {
+                act = true; ex = X; T = V & (~0u << (e - s));
+            } else {
+                act = true; T = 0;
+                uint32_t t = e;
+                while (t < se && !((V >> (t - s)) & 1u)) { T |= 1u << (t - s); t += step[t - t0]; }
+                if (t < se) { ex = X; T |= V & (~0u << (t - s)); }
+                else ex = t;
+            }
+            Ys[tid] = ex;
+            // nearest active segment <= tid: highest set bit of the wave's ballot at or
+            // below this lane, else the last active segment of an earlier wave
+            const uint64_t am = __ballot(act);
+            const uint32_t lane = tid & 63;
+            if (lane == 0) s_red[tid >> 6] = am ? (tid & ~63u) + 64 - (uint32_t)__clzll(am) : 0u;
+            __syncthreads();
+            const uint64_t le = am & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+            uint32_t li = le ? (tid & ~63u) + 64 - (uint32_t)__clzll(le) : 0u;
+            for (int w = (int)(tid >> 6) - 1; w >= 0 && !li; w--) li = s_red[w];
+            const uint32_t ne = li ? Ys[li - 1] : Gs[tid + 1];
+            if (ne != Gs[tid + 1]) { Gs[tid + 1] = ne; s_chg[r & 1] = 1; }
+            if (tid == 0) s_chg[(r + 1) & 1] = 0;
+            __syncthreads();
+            if (!s_chg[r & 1]) break;
+        }
+        if (dbg & 256u) return;   // timing: + Jacobi rounds
     }
-    if (dbg & 256u) return;   // timing: + Jacobi rounds
     // counts of this lane's chain positions, prefix over lanes
     uint32_t cnt[3] = {(uint32_t)__builtin_popcount(T), 0, 0};
     for (uint32_t bits = T; bits; bits &= bits - 1) {
@@ -794,7 +839,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         pre[q] = p + inc[q] - cnt[q];
         tot[q] = a;
     }
-    if (!dense) {
+    if (!dense && !uniform_tile()) {
         // compact match list: the speculative chain's match tokens in order (m values
         // from the search results); with m rows only in the first kResolveSpan
         // positions, k_emit takes the rest of the tile's matches from here
@@ -817,7 +862,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     if (tid == 0) {
         const uint32_t nsub = (t1 - t0 + kSeg - 1) / kSeg;
-        ti[0] = dense ? kTileMFull : 0u;   // dense: the run table wrote m for every position
+        // dense: the run table wrote m for every position; uniform: m_uniform everywhere
+        ti[0] = uniform_tile() ? (kTileUniform | kTileMFull) : dense ? kTileMFull : 0u;
         ti[1] = Gs[nsub];
         ti[2] = tot[0];
         ti[3] = tot[1];

@@ -91,7 +91,7 @@ struct Cnt3 {
 // counts of the speculative chain positions in [t0, t0 + rel): k_match's prefix
 // for the word plus the set bits of the (original) word below rel.  Wave-wide.
 __device__ Cnt3 spec_prefix(const uint64_t *pfx, const uint32_t *mt, const uint64_t *mb, uint64_t orig_word,
-                            uint32_t rel) {
+                            uint32_t rel, bool uni, uint32_t t0, uint32_t blen) {
     const uint32_t lane = lane_id();
     const uint32_t w = rel >> 6, r = rel & 63;
     const uint64_t p = pfx[w];
@@ -99,7 +99,7 @@ __device__ Cnt3 spec_prefix(const uint64_t *pfx, const uint32_t *mt, const uint6
     const uint64_t below = r ? (orig_word & ((1ull << r) - 1)) : 0ull;
     uint32_t mt_ = 0, gb = 0;
     if ((below >> lane) & (mb[w] >> lane) & 1ull) {
-        const uint32_t L = m_len(mt[w * 64 + lane]);
+        const uint32_t L = m_len(uni ? m_uniform(t0 + w * 64 + lane, blen) : mt[w * 64 + lane]);
         if (L) { mt_ = 1; gb = (L >> 2) + 3; }
     }
     c.tok += (uint32_t)__popcll(below);
@@ -159,6 +159,7 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     uint64_t *out = fp + 8ull * tix;
     const uint32_t *ti = tinfo + 8ull * tix;
     bool ok = (ti[0] & kTileLazy) == 0;
+    const bool uni = (ti[0] & kTileUniform) != 0;   // m = m_uniform, no rows
     uint32_t ea = t0;
     if (ok && k > 0) {
         const uint32_t *tp = tinfo + 8ull * (tix - 1);
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     for (uint32_t q = 0; q < 4; q++) {
         const uint32_t x = 64 * q + lane;
         const uint64_t mbq = __shfl(mv, q, 64);
-        mreg[q] = (x < t1 - t0 && ((mbq >> lane) & 1ull)) ? mt[x] : 0u;
+        mreg[q] = (x < t1 - t0 && ((mbq >> lane) & 1ull)) ? (uni ? m_uniform(t0 + x, blen) : mt[x]) : 0u;
     }
     uint64_t orig[4], mbw[4], nwb[4];
 #pragma unroll
@@ -221,7 +222,8 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     uint32_t keep_from = rel;   // speculative bits at positions >= keep_from stay
     uint32_t convrec = kConvAll;
     if (conv) {
-        const Cnt3 drop = rel ? spec_prefix(chain_pfx + (uint64_t)tix * (kTile / 64), mt, mb, orig[rel >> 6], rel)
+        const Cnt3 drop = rel ? spec_prefix(chain_pfx + (uint64_t)tix * (kTile / 64), mt, mb, orig[rel >> 6], rel, uni,
+                                            t0, blen)
                               : Cnt3{0, 0, 0};
         fin.tok += ti[2] - drop.tok;
         fin.mat += ti[3] - drop.mat;
@@ -316,6 +318,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         }
         const bool lazy = (sti[j][0] & kTileLazy) != 0;
         const bool mfull = (sti[j][0] & kTileMFull) != 0;   // else m[] rows stop at kResolveSpan
+        const bool uni = (sti[j][0] & kTileUniform) != 0;  // m = m_uniform, no rows
         uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
         const uint64_t *pfx = chain_pfx + (uint64_t)tix * (kTile / 64);
         const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
@@ -325,6 +328,26 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         if (e >= t1) {  // a match spans the whole tile
             for (uint32_t w = lane; w < nw; w += 64) cw[w] = 0;
             if (lane == 0) tconv[tix] = kConvAll;
+            continue;
+        }
+        if (uni) {
+            // one byte value: the chain from e follows from m_uniform.  Every lane walks it
+            // to the tile end (<= 17 tokens, ALU only) counting the tokens and keeping the
+            // bits of its chain word
+            Cnt3 w{0, 0, 0};
+            uint64_t wv = 0;
+            const uint32_t lo = t0 + 64 * lane;
+            uint32_t t = e;
+            while (t < t1) {
+                const uint32_t Lm = m_len(m_uniform(t, blen));
+                w.add(Lm);
+                if (t - lo < 64) wv |= 1ull << (t - lo);
+                t += Lm + 1;
+            }
+            if (lane < nw) cw[lane] = wv;
+            if (lane == 0) tconv[tix] = kConvAll;
+            run.tok += w.tok; run.mat += w.mat; run.gb += w.gb;
+            e = t;
             continue;
         }
         const Cnt3 tot{sti[j][2], sti[j][3], sti[j][4]};
@@ -364,7 +387,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                                                       : 0u;
             }
             pk = 0xFFFFFFFFu;
-            if (k + 1 < ntiles && j + 1 < 64 && (sti[j + 1][0] & kTileMFull)) {
+            if (k + 1 < ntiles && j + 1 < 64 && (sti[j + 1][0] & (kTileMFull | kTileUniform)) == kTileMFull) {
                 const uint32_t u0 = t1, u1 = min(blen, u0 + kTile);
                 fetch_tile(m + bstart + u0, mb + kTile / 64, cw + kTile / 64, u1 - u0, (u1 - u0 + 63) / 64, pv, pmb, pcw);
                 pk = k + 1;
@@ -387,7 +410,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
             const uint32_t rel = t - t0;
             if (!lazy && ((bmL[rel >> 6] >> (rel & 63)) & 1ull)) {
                 // converged: the speculative chain from here on is the true one
-                const Cnt3 drop = mfull ? spec_prefix(pfx, mt, mb, cw[rel >> 6], rel)
+                const Cnt3 drop = mfull ? spec_prefix(pfx, mt, mb, cw[rel >> 6], rel, false, t0, blen)
                                         : spec_prefix_c(pfx, mtok + (uint64_t)tix * kTileMatches, mb, cw[rel >> 6], rel);
                 if (!mfull) convrec = rel | (drop.mat << 16);
                 walked.tok += tot.tok - drop.tok;
@@ -543,7 +566,7 @@ constexpr uint32_t kInW = (kTile + kLookAhead) / 4 + 2;   // tile input + look-a
 __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
                                               const uint64_t *__restrict__ mbits, const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
                                               const BlockInfo *__restrict__ binfo, const uint32_t *__restrict__ mtok,
-                                              const uint32_t *__restrict__ tconv,
+                                              const uint32_t *__restrict__ tconv, const uint32_t *__restrict__ tinfo,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb) {
     __shared__ uint32_t sh[16];
@@ -565,6 +588,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     const uint32_t tk1 = last ? binfo[b].ntok : tile_off[3 * tix + 3];
     const uint32_t mk1 = last ? binfo[b].nmatch : tile_off[3 * tix + 4];
     const uint32_t cv = tconv[tix];
+    const bool uni = (tinfo[8 * tix] & kTileUniform) != 0;   // m = m_uniform, no rows
     const uint32_t s = t0 + tid * 16;   // this lane's 16 positions: one quarter of a chain word
     uint64_t cwv = 0, mbv = 0;
     if (s < t1) {
@@ -629,7 +653,10 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     // ---- round 2: m rows and the compact list ----
     const uint32_t *mt = m + bstart + s;
     uint32_t mm[16];
-    if (rd && ((uintptr_t)mt & 15) == 0) {   // whole 64-B row as four 16-B loads
+    if (uni) {
+#pragma unroll
+        for (uint32_t q = 0; q < 16; q++) mm[q] = ((rd >> q) & 1u) ? m_uniform(s + q, blen) : 0u;
+    } else if (rd && ((uintptr_t)mt & 15) == 0) {   // whole 64-B row as four 16-B loads
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
             const uint4 w4 = ((const uint4 *)mt)[q];
@@ -753,7 +780,7 @@ void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_
                        tile_off, tconv, binfo);
     if (ev) (void)hipEventRecord(ev[0], st);
     hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok, tconv,
-                       s_flags, s_chars, s_p, s_golomb);
+                       tinfo, s_flags, s_chars, s_p, s_golomb);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 
