@@ -359,40 +359,69 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
     }
 }
 
-// ---- uniform tiles (one byte value over the whole image): m = m_uniform ----
-// step and mbits of the tile's positions (mbw: the block's mbits words)
-__device__ inline void uniform_step(uint16_t *step, uint64_t *mbw, uint32_t *s_match, uint32_t t0, uint32_t t1,
-                                          uint32_t blen) {
-    const uint32_t tid = threadIdx.x;
-    bool any = false;
+// ---- uniform tiles (one byte value over the whole image: zeros) ----
+// m is m_uniform everywhere: no search, no run table, no m[] rows.  The speculative chain
+// from t0 follows directly; this publishes what the parse below publishes for other tiles
+// (mbits, chain words, per-word prefix counts, tile info with kTileUniform).
+__device__ inline void uniform_tile_out(uint32_t *sc /* >= kMT + 1 words */, uint32_t *s_red, uint64_t *mbw,
+                                        uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t t0, uint32_t t1,
+                                        uint32_t blen) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    auto ustep = [&](uint32_t p) -> uint32_t { return m_len(m_uniform(p, blen)) + 1; };
 #pragma unroll
-    for (uint32_t r = 0; r < kQPL; r++) {
-        const uint32_t rel = tid + kMT * r, i = t0 + rel;
-        const uint32_t mu = i < t1 ? m_uniform(i, blen) : 0u;
-        step[rel] = (uint16_t)(mu ? m_len(mu) + 1 : 1);
-        any = any || mu != 0;
-        const uint64_t mb = __ballot(mu != 0);
-        if ((tid & 63) == 0 && i < t1) mbw[i >> 6] = mb;
+    for (uint32_t r = 0; r < kQPL; r++) {   // a wave's 64 lanes: 64 consecutive positions
+        const uint32_t i = t0 + tid + kMT * r;
+        const uint64_t mb = __ballot(i < t1 && m_uniform(i, blen) != 0);
+        if (lane == 0 && i < t1) mbw[i >> 6] = mb;
     }
-    if (any) *s_match = 1;
-    __syncthreads();
-}
-
-// the speculative chain from t0 follows from m_uniform: every lane walks it (<= 17
-// tokens to its sub-segment [s, se)); returns the lane's chain bits, the lane holding
-// the tile's last position writes the exit to Gs[nsub]
-__device__ inline uint32_t uniform_chain(uint32_t *Gs, uint32_t s, uint32_t se, uint32_t t0, uint32_t t1,
-                                               uint32_t blen) {
-    auto ustep = [&](uint32_t p) -> uint32_t {
-        const uint32_t mu = m_uniform(p, blen);
-        return mu ? m_len(mu) + 1 : 1u;
-    };
+    const uint32_t s = t0 + tid * kSeg, se = min(s + kSeg, t1);
     uint32_t T = 0, p = t0;
     while (p < s) p += ustep(p);
-    while (p < se) { T |= 1u << (p - s); p += ustep(p); }
-    if (s < t1 && se == t1) Gs[(t1 - t0 + kSeg - 1) / kSeg] = p;
+    uint32_t cnt[3] = {0, 0, 0};
+    while (p < se) {
+        T |= 1u << (p - s);
+        const uint32_t Lm = ustep(p) - 1;
+        cnt[0]++;
+        if (Lm) { cnt[1]++; cnt[2] += (Lm >> 2) + 3; }
+        p += Lm + 1;
+    }
+    if (s < t1 && se == t1) sc[kMT] = p;   // the tile's exit
+    uint32_t inc[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) inc[q] = wave_incl_scan(cnt[q]);
+    if (lane == 63)
+        for (int q = 0; q < 3; q++) s_red[q * kWaves + wv] = inc[q];
+    sc[tid] = T;
     __syncthreads();
-    return T;
+    uint32_t pre[3], tot[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        uint32_t a = 0, b = 0;
+        for (uint32_t w = 0; w < kWaves; w++) {
+            const uint32_t v = s_red[q * kWaves + w];
+            if (w < wv) a += v;
+            b += v;
+        }
+        pre[q] = a + inc[q] - cnt[q];
+        tot[q] = b;
+    }
+    constexpr uint32_t kLanesPerWord = 64 / kSeg;
+    const uint32_t nwords = (t1 - t0 + 63) / 64;
+    if ((tid % kLanesPerWord) == 0 && tid / kLanesPerWord < nwords) {
+        const uint32_t w = tid / kLanesPerWord;
+        uint64_t word = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kLanesPerWord; q++) word |= (uint64_t)sc[tid + q] << (kSeg * q);
+        cw[w] = word;
+        pfx[w] = (uint64_t)pre[0] | ((uint64_t)pre[1] << 13) | ((uint64_t)pre[2] << 24);
+    }
+    if (tid == 0) {
+        ti[0] = kTileUniform | kTileMFull;
+        ti[1] = sc[kMT];
+        ti[2] = tot[0];
+        ti[3] = tot[1];
+        ti[4] = tot[2];
+    }
 }
 
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
@@ -504,9 +533,6 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     __syncthreads();
     const bool rmode = (s_nruns <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
-    // one byte value over the whole image (zeros): m is m_uniform, no search, no m[] rows.
-    // Re-read from LDS where used (nothing held in registers across the search)
-    auto uniform_tile = [&]() -> bool { return s_nruns == 1 && !(dbg & 12u); };
     if (dbg & 16u) return;   // timing: staging + run count only
 
     // this lane's 12 consecutive window positions 12 tid .. 12 tid + 11 take their keys from
@@ -520,9 +546,13 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         return key_mix(__builtin_amdgcn_alignbyte(kw[(r >> 2) + 1], kw[r >> 2], r & 3) & 0xFFFFFFu);
     };
 
-    if (uniform_tile()) {
-        uniform_step(step, mbits + (uint64_t)b * L.wpb, &s_match, t0, t1, blen);
-    } else if (rmode) {
+    if (rmode) {
+        if (s_nruns == 1 && !(dbg & 12u)) {   // one byte value over the whole image (zeros)
+            uniform_tile_out(region, s_red, mbits + (uint64_t)b * L.wpb,
+                             chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64),
+                             chain_pfx + (uint64_t)blockIdx.x * (kTile / 64), tinfo + 8ull * blockIdx.x, t0, t1, blen);
+            return;
+        }
         for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
         if (tid == 0) s_unknown = 1;
         __syncthreads();
@@ -760,59 +790,55 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     uint32_t *Vs = Xs + kMT;
     const uint32_t s = t0 + tid * kSeg;
     const uint32_t se = min(s + kSeg, t1);
+    uint32_t V = 0, X = s;
     uint32_t T = 0;
-    if (uniform_tile()) {
-        T = uniform_chain(Gs, s, se, t0, t1, blen);
-    } else {
-        uint32_t V = 0, X = s;
-        uint32_t *Ys = Vs;   // exits of a Jacobi round (Vs is free until the counts below)
-        if (s < t1) {
-            uint32_t t = s;
-            while (t < se) { V |= 1u << (t - s); t += step[t - t0]; }
-            X = t;
-        }
-        Xs[tid] = X;
-        Gs[tid + 1] = X;
-        if (tid == 0) Gs[0] = t0;
-        __syncthreads();
-        if (dbg & 512u) return;   // timing: + sub-segment walks
-        // Jacobi rounds.  A segment is active when its entry lies inside it; the next
-        // entry of segment k + 1 is the exit of the nearest active segment <= k (a
-        // block-wide running max of active indices), so a long token passes over any
-        // number of segments in one round.
-        for (uint32_t r = 0;; r++) {
-            const uint32_t e = Gs[tid];
-            uint32_t ex;
-            bool act = false;
-            if (s >= t1 || e >= se) {
-                ex = e; T = 0;
-            } else if ((V >> (e - s)) & 1u) {
-                act = true; ex = X; T = V & (~0u << (e - s));
-            } else {
-                act = true; T = 0;
-                uint32_t t = e;
-                while (t < se && !((V >> (t - s)) & 1u)) { T |= 1u << (t - s); t += step[t - t0]; }
-                if (t < se) { ex = X; T |= V & (~0u << (t - s)); }
-                else ex = t;
-            }
-            Ys[tid] = ex;
-            // nearest active segment <= tid: highest set bit of the wave's ballot at or
-            // below this lane, else the last active segment of an earlier wave
-            const uint64_t am = __ballot(act);
-            const uint32_t lane = tid & 63;
-            if (lane == 0) s_red[tid >> 6] = am ? (tid & ~63u) + 64 - (uint32_t)__clzll(am) : 0u;
-            __syncthreads();
-            const uint64_t le = am & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-            uint32_t li = le ? (tid & ~63u) + 64 - (uint32_t)__clzll(le) : 0u;
-            for (int w = (int)(tid >> 6) - 1; w >= 0 && !li; w--) li = s_red[w];
-            const uint32_t ne = li ? Ys[li - 1] : Gs[tid + 1];
-            if (ne != Gs[tid + 1]) { Gs[tid + 1] = ne; s_chg[r & 1] = 1; }
-            if (tid == 0) s_chg[(r + 1) & 1] = 0;
-            __syncthreads();
-            if (!s_chg[r & 1]) break;
-        }
-        if (dbg & 256u) return;   // timing: + Jacobi rounds
+    uint32_t *Ys = Vs;   // exits of a Jacobi round (Vs is free until the counts below)
+    if (s < t1) {
+        uint32_t t = s;
+        while (t < se) { V |= 1u << (t - s); t += step[t - t0]; }
+        X = t;
     }
+    Xs[tid] = X;
+    Gs[tid + 1] = X;
+    if (tid == 0) Gs[0] = t0;
+    __syncthreads();
+    if (dbg & 512u) return;   // timing: + sub-segment walks
+    // Jacobi rounds.  A segment is active when its entry lies inside it; the next
+    // entry of segment k + 1 is the exit of the nearest active segment <= k (a
+    // block-wide running max of active indices), so a long token passes over any
+    // number of segments in one round.
+    for (uint32_t r = 0;; r++) {
+        const uint32_t e = Gs[tid];
+        uint32_t ex;
+        bool act = false;
+        if (s >= t1 || e >= se) {
+            ex = e; T = 0;
+        } else if ((V >> (e - s)) & 1u) {
+            act = true; ex = X; T = V & (~0u << (e - s));
+        } else {
+            act = true; T = 0;
+            uint32_t t = e;
+            while (t < se && !((V >> (t - s)) & 1u)) { T |= 1u << (t - s); t += step[t - t0]; }
+            if (t < se) { ex = X; T |= V & (~0u << (t - s)); }
+            else ex = t;
+        }
+        Ys[tid] = ex;
+        // nearest active segment <= tid: highest set bit of the wave's ballot at or
+        // below this lane, else the last active segment of an earlier wave
+        const uint64_t am = __ballot(act);
+        const uint32_t lane = tid & 63;
+        if (lane == 0) s_red[tid >> 6] = am ? (tid & ~63u) + 64 - (uint32_t)__clzll(am) : 0u;
+        __syncthreads();
+        const uint64_t le = am & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        uint32_t li = le ? (tid & ~63u) + 64 - (uint32_t)__clzll(le) : 0u;
+        for (int w = (int)(tid >> 6) - 1; w >= 0 && !li; w--) li = s_red[w];
+        const uint32_t ne = li ? Ys[li - 1] : Gs[tid + 1];
+        if (ne != Gs[tid + 1]) { Gs[tid + 1] = ne; s_chg[r & 1] = 1; }
+        if (tid == 0) s_chg[(r + 1) & 1] = 0;
+        __syncthreads();
+        if (!s_chg[r & 1]) break;
+    }
+    if (dbg & 256u) return;   // timing: + Jacobi rounds
     // counts of this lane's chain positions, prefix over lanes
     uint32_t cnt[3] = {(uint32_t)__builtin_popcount(T), 0, 0};
     for (uint32_t bits = T; bits; bits &= bits - 1) {
@@ -839,7 +865,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         pre[q] = p + inc[q] - cnt[q];
         tot[q] = a;
     }
-    if (!dense && !uniform_tile()) {
+    if (!dense) {
         // compact match list: the speculative chain's match tokens in order (m values
         // from the search results); with m rows only in the first kResolveSpan
         // positions, k_emit takes the rest of the tile's matches from here
@@ -862,8 +888,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     if (tid == 0) {
         const uint32_t nsub = (t1 - t0 + kSeg - 1) / kSeg;
-        // dense: the run table wrote m for every position; uniform: m_uniform everywhere
-        ti[0] = uniform_tile() ? (kTileUniform | kTileMFull) : dense ? kTileMFull : 0u;
+        ti[0] = dense ? kTileMFull : 0u;   // dense: the run table wrote m for every position
         ti[1] = Gs[nsub];
         ti[2] = tot[0];
         ti[3] = tot[1];
