@@ -839,11 +839,21 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if (!s_chg[r & 1]) break;
     }
     if (dbg & 256u) return;   // timing: + Jacobi rounds
-    // counts of this lane's chain positions, prefix over lanes
+    // counts of this lane's chain positions, prefix over lanes.  The lane's 8 steps come
+    // in one 16-B LDS read (no serial read per chain position)
+    static_assert(kSeg == 8, "one uint4 of u16 steps per lane");
+    uint32_t stp[kSeg];
+    {
+        const uint4 st4 = ((const uint4 *)step)[tid];
+        const uint32_t w4[4] = {st4.x, st4.y, st4.z, st4.w};
+#pragma unroll
+        for (uint32_t q = 0; q < kSeg; q++) stp[q] = (w4[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+    }
     uint32_t cnt[3] = {(uint32_t)__builtin_popcount(T), 0, 0};
-    for (uint32_t bits = T; bits; bits &= bits - 1) {
-        const uint32_t Lm = step[s - t0 + __builtin_ctz(bits)] - 1u;
-        if (Lm) { cnt[1]++; cnt[2] += (Lm >> 2) + 3; }
+#pragma unroll
+    for (uint32_t q = 0; q < kSeg; q++) {
+        const uint32_t Lm = stp[q] - 1u;
+        if (((T >> q) & 1u) && Lm) { cnt[1]++; cnt[2] += (Lm >> 2) + 3; }
     }
     const uint32_t lane = tid & 63, wv = tid >> 6;
     uint32_t inc[3];
@@ -865,17 +875,18 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         pre[q] = p + inc[q] - cnt[q];
         tot[q] = a;
     }
+    if (dbg & 1024u) return;   // timing: + counts and their scan
     if (!dense) {
         // compact match list: the speculative chain's match tokens in order (m values
         // from the search results); with m rows only in the first kResolveSpan
         // positions, k_emit takes the rest of the tile's matches from here
         const uint32_t *res_lds = region + kResLds;
         uint32_t *mt = mtok + (uint64_t)blockIdx.x * kTileMatches + pre[1];
-        for (uint32_t bits = T; bits; bits &= bits - 1) {
-            const uint32_t rel = s - t0 + __builtin_ctz(bits);
-            if (step[rel] > 1) *mt++ = res_lds[rel];
-        }
+#pragma unroll
+        for (uint32_t q = 0; q < kSeg; q++)
+            if (((T >> q) & 1u) && stp[q] > 1) *mt++ = res_lds[s - t0 + q];
     }
+    if (dbg & 2048u) return;   // timing: + compact list
     constexpr uint32_t kLanesPerWord = 64 / kSeg;   // 8
     if ((tid % kLanesPerWord) == 0 && tid / kLanesPerWord < nwords) {
         const uint32_t w = tid / kLanesPerWord;
