@@ -281,18 +281,24 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
         uint64_t *mbl = (uint64_t *)(region + kSpMb);
         for (uint32_t x = tid; x < kTile / 2; x += kMT) region[x] = 0x00010001u;   // step = 1 (literal)
         for (uint32_t x = tid; x <= kSparseBuckets / 2; x += kMT) cnt[x] = 0;
+        // the 12 dup tests (independent LDS reads), then one slot reservation per wave
+        uint32_t fm = 0;   // bit r: key r's hash repeats
 #pragma unroll
         for (uint32_t r = 0; r < kIns; r++) {
-            const uint32_t x = kIns * tid + r;
             const uint32_t hf = hash_of(r) >> (24 - kFilterBits);
-            const bool f = x < ins_end && ((dupm[hf >> 5] >> (hf & 31)) & 1u);
-            const uint64_t bal = __ballot(f);
-            if (bal) {
-                uint32_t base = 0;
-                if ((tid & 63) == 0) base = atomicAdd(s_np, (uint32_t)__popcll(bal));
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (f) P[base + lanes_below(bal)] = x | (hf << 13);
-            }
+            if (kIns * tid + r < ins_end && ((dupm[hf >> 5] >> (hf & 31)) & 1u)) fm |= 1u << r;
+        }
+        const uint32_t nf = (uint32_t)__builtin_popcount(fm);
+        const uint32_t incf = wave_incl_scan(nf);
+        uint32_t base = 0;
+        if ((tid & 63) == 63 && incf) base = atomicAdd(s_np, incf);
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, 63) + incf - nf;
+        for (uint32_t bits = fm; bits; bits &= bits - 1) {
+            const uint32_t r = __builtin_ctz(bits);
+            const uint32_t x = kIns * tid + r;
+            const uint32_t key = lds_key3(sdw, x);
+            const uint32_t hf = key_mix(key) >> (24 - kFilterBits);
+            P[base++] = x | (hf << 13);
         }
         __syncthreads();
         const uint32_t np = *s_np;
@@ -572,16 +578,25 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     if (tid == 0) { s_events = 0; s_np = 0; }
     __syncthreads();
     {
+        // all 12 "seen" atomics in flight at once (program order keeps a lane's own
+        // repeats visible to it), then the "dup" marks without return values
+        uint32_t old[kIns];
+#pragma unroll
+        for (uint32_t r = 0; r < kIns; r++) {
+            old[r] = 0;
+            if (kIns * tid + r < ins_end) {
+                const uint32_t hf = hash_of(r) >> (24 - kFilterBits);
+                old[r] = atomicOr(&seen[hf >> 5], 1u << (hf & 31));
+            }
+        }
         uint32_t ev = 0;
 #pragma unroll
         for (uint32_t r = 0; r < kIns; r++) {
-            if (kIns * tid + r < ins_end) {
-                const uint32_t hf = hash_of(r) >> (24 - kFilterBits);
-                const uint32_t bit = 1u << (hf & 31);
-                if (atomicOr(&seen[hf >> 5], bit) & bit) {
-                    atomicOr(&dupm[hf >> 5], bit);
-                    ev++;
-                }
+            const uint32_t hf = hash_of(r) >> (24 - kFilterBits);
+            const uint32_t bit = 1u << (hf & 31);
+            if (kIns * tid + r < ins_end && (old[r] & bit)) {
+                atomicOr(&dupm[hf >> 5], bit);
+                ev++;
             }
         }
         ev = wave_sum_u32(ev);
