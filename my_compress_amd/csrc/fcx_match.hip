@@ -603,6 +603,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if ((tid & 63) == 0 && ev) atomicAdd(&s_events, ev);
     }
     __syncthreads();
+    if (dbg & 4096u) return;   // timing: + repeat filter
     sparse = s_events <= kSparseEvents;
     }   // repeat filter
 
