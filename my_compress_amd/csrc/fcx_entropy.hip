@@ -128,17 +128,22 @@ __global__ __launch_bounds__(kEncT) void k_hist(Layout L, const BlockInfo *__res
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_tree(Layout L, const uint32_t *__restrict__ hist,
-                                             BlockInfo *__restrict__ binfo, uint32_t *__restrict__ ctab,
-                                             uint8_t *__restrict__ ltab, uint8_t *__restrict__ hhdr,
-                                             uint32_t *__restrict__ chunk_off, uint32_t *__restrict__ err) {
-    __shared__ uint32_t w[256], sw[256], ss[256];
+constexpr uint32_t kTreeT = 256;   // k_tree workgroup: one thread per symbol / per chunk
+
+__global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__restrict__ hist,
+                                                 BlockInfo *__restrict__ binfo, uint32_t *__restrict__ ctab,
+                                                 uint8_t *__restrict__ ltab, uint8_t *__restrict__ hhdr,
+                                                 uint32_t *__restrict__ chunk_off, uint32_t *__restrict__ err) {
+    __shared__ __attribute__((aligned(16))) uint32_t w[256];
+    __shared__ uint32_t sw[256], ss[256], ln[256];
     __shared__ uint32_t iw[256], il[256], ir[256], par[512];
-    const uint32_t lane = threadIdx.x;
+    __shared__ uint32_t part[4][256];
+    __shared__ uint32_t s_red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / kStreams, s = blockIdx.x % kStreams;
     BlockInfo &bi = binfo[b];
     if (!stream_active(bi, s)) {
-        if (lane == 0) { bi.hdrlen[s] = 0; bi.nwords[s] = 0; }
+        if (tid == 0) { bi.hdrlen[s] = 0; bi.nwords[s] = 0; }
         return;
     }
     const uint32_t hb = (b * kStreams + s) * 256;
@@ -146,45 +151,45 @@ __global__ __launch_bounds__(64) void k_tree(Layout L, const uint32_t *__restric
     for (uint32_t q = 0; q < s; q++) r0 += L.cpb[q];
     const uint32_t nch = (bi.slen[s] + kChunk - 1) / kChunk;
     const uint32_t *hc = hist + ((uint64_t)b * L.cpb_total + r0) * 256;   // this stream's chunk histograms
-    uint32_t acc[4] = {0, 0, 0, 0};
+    {   // symbol weights: wave wv sums the chunks c = wv mod 4 (lane: symbols lane + 64 q)
+        uint32_t acc[4] = {0, 0, 0, 0};
 #pragma unroll 8
-    for (uint32_t c = 0; c < nch; c++)
+        for (uint32_t c = wv; c < nch; c += 4)
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) acc[q] += hc[c * 256 + lane + 64 * q];
-    uint32_t real = 0;
+            for (uint32_t q = 0; q < 4; q++) acc[q] += hc[c * 256 + lane + 64 * q];
 #pragma unroll
-    for (uint32_t q = 0; q < 4; q++) {
-        w[lane + 64 * q] = acc[q];
-        real += (uint32_t)__popcll(__ballot(acc[q] != 0));
+        for (uint32_t q = 0; q < 4; q++) part[wv][lane + 64 * q] = acc[q];
     }
     __syncthreads();
+    const uint32_t wt = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    w[tid] = wt;
+    const uint32_t real = (uint32_t)__syncthreads_count(wt != 0);
     // stable sort of the leaves by (weight, symbol): rank = number of smaller keys
+    if (wt) {
+        const uint64_t key = ((uint64_t)wt << 8) | tid;
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < 256; j += 4) {
+            const uint4 w4 = *(const uint4 *)&w[j];
+            const uint32_t wj[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-    for (uint32_t q = 0; q < 4; q++) {
-        const uint32_t sym = lane + 64 * q, wt = w[sym];
-        if (wt) {
-            const uint64_t key = ((uint64_t)wt << 8) | sym;
-            uint32_t rank = 0;
-            for (uint32_t j = 0; j < 256; j++) {
-                const uint32_t wj = w[j];
-                rank += (wj != 0 && (((uint64_t)wj << 8) | j) < key) ? 1u : 0u;
-            }
-            sw[rank] = wt;
-            ss[rank] = sym;
+            for (uint32_t u = 0; u < 4; u++)
+                rank += (wj[u] != 0 && (((uint64_t)wj[u] << 8) | (j + u)) < key) ? 1u : 0u;
         }
+        sw[rank] = wt;
+        ss[rank] = tid;
     }
     __syncthreads();
     const uint32_t nint = real >= 2 ? real - 1 : 0;
-    if (lane == 0 && nint) {
+    if (tid == 0 && nint) {
         // two-queue merge == the reference's sorted-list re-insertion (570-611)
         uint32_t lq = 0, iq = 0;
         for (uint32_t kk = 0; kk < nint; kk++) {
-            uint32_t id[2], wt[2];
+            uint32_t id[2], wq[2];
             for (int h = 0; h < 2; h++) {
-                if (lq < real && (iq >= kk || sw[lq] <= iw[iq])) { id[h] = ss[lq]; wt[h] = sw[lq]; lq++; }
-                else { id[h] = 256 + iq; wt[h] = iw[iq]; iq++; }
+                if (lq < real && (iq >= kk || sw[lq] <= iw[iq])) { id[h] = ss[lq]; wq[h] = sw[lq]; lq++; }
+                else { id[h] = 256 + iq; wq[h] = iw[iq]; iq++; }
             }
-            iw[kk] = wt[0] + wt[1];
+            iw[kk] = wq[0] + wq[1];
             il[kk] = id[0];
             ir[kk] = id[1];
             par[id[0]] = 256 + kk;
@@ -193,13 +198,10 @@ __global__ __launch_bounds__(64) void k_tree(Layout L, const uint32_t *__restric
     }
     __syncthreads();
     const uint32_t root = 256 + nint - 1;
-    uint32_t myl[4];
-#pragma unroll
-    for (uint32_t q = 0; q < 4; q++) {
-        const uint32_t sym = lane + 64 * q;
+    {   // code of symbol tid: root -> leaf path, root decision in bit 0
         uint32_t code = 0, len = 0;
-        if (nint && w[sym]) {
-            uint32_t cur = sym;
+        if (nint && wt) {
+            uint32_t cur = tid;
             while (cur != root && len <= 32) {
                 const uint32_t p = par[cur];
                 code = (code << 1) | (ir[p - 256] == cur ? 1u : 0u);
@@ -208,43 +210,60 @@ __global__ __launch_bounds__(64) void k_tree(Layout L, const uint32_t *__restric
             }
             if (len > 32) atomicOr(err, kErrCodeLen);
         }
-        ctab[hb + sym] = code;
-        ltab[hb + sym] = (uint8_t)len;
-        myl[q] = len;
+        ctab[hb + tid] = code;
+        ltab[hb + tid] = (uint8_t)len;
+        ln[tid] = len;
     }
-    // starting bit of every chunk: chunk histogram . code lengths, scanned in chunk order
-    uint64_t bits = 0;
-    for (uint32_t c = 0; c < nch; c++) {
-        uint32_t part = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < 4; q++) part += hc[c * 256 + lane + 64 * q] * myl[q];
-        part = wave_sum_u32(part);
-        if (lane == 0) chunk_off[(uint64_t)b * L.cpb_total + r0 + c] = (uint32_t)bits;
-        bits += part;
+    __syncthreads();
+    // starting bit of every chunk: chunk histogram . code lengths (thread c: chunk c, its
+    // 256 counts in 64 independent 16-B loads), exclusive scan in chunk order
+    uint64_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nch; c0 += kTreeT) {
+        const uint32_t c = c0 + tid;
+        uint32_t bitsc = 0;
+        if (c < nch) {
+            const uint4 *h4 = (const uint4 *)(hc + (uint64_t)c * 256);
+#pragma unroll 16
+            for (uint32_t q = 0; q < 64; q++) {
+                const uint4 v = h4[q];
+                bitsc += v.x * ln[4 * q] + v.y * ln[4 * q + 1] + v.z * ln[4 * q + 2] + v.w * ln[4 * q + 3];
+            }
+        }
+        const uint32_t inc = wave_incl_scan(bitsc);
+        if (lane == 63) s_red[wv] = inc;
+        __syncthreads();
+        uint32_t pre = 0, all = 0;
+        for (uint32_t q = 0; q < 4; q++) {
+            if (q < wv) pre += s_red[q];
+            all += s_red[q];
+        }
+        if (c < nch) chunk_off[(uint64_t)b * L.cpb_total + r0 + c] = (uint32_t)(carry + pre + inc - bitsc);
+        carry += all;
+        __syncthreads();
     }
     // header: [u8 ts][ceil(2ts/8) B internal-child bitmap][ts x (u8 l, u8 r)]
     const uint32_t ts = nint, nbm = (2 * ts + 7) / 8;
     uint8_t *hdr = hhdr + (uint64_t)(b * kStreams + s) * kHuffHdrStride;
-    if (lane == 0) hdr[0] = (uint8_t)ts;
-    if (lane < nbm) {
+    if (tid == 0) hdr[0] = (uint8_t)ts;
+    if (tid < nbm) {
         uint32_t byte = 0;
         for (uint32_t q = 0; q < 8; q++) {
-            const uint32_t node = (8 * lane + q) >> 1;
+            const uint32_t node = (8 * tid + q) >> 1;
             if (node < ts) {
                 const uint32_t ch = (q & 1) ? ir[node] : il[node];
                 if (ch >= 256) byte |= 1u << q;
             }
         }
-        hdr[1 + lane] = (uint8_t)byte;
+        hdr[1 + tid] = (uint8_t)byte;
     }
-    for (uint32_t kk = lane; kk < ts; kk += 64) {
+    for (uint32_t kk = tid; kk < ts; kk += kTreeT) {
         const uint32_t l = il[kk], r = ir[kk];
         hdr[1 + nbm + 2 * kk] = (uint8_t)(l >= 256 ? (256 - real) + (l - 256) : l);
         hdr[1 + nbm + 2 * kk + 1] = (uint8_t)(r >= 256 ? (256 - real) + (r - 256) : r);
     }
-    if (lane == 0) {
+    if (tid == 0) {
         bi.hdrlen[s] = 1 + nbm + 2 * ts;
-        bi.nwords[s] = (uint32_t)((bits + 31) / 32);
+        bi.nwords[s] = (uint32_t)((carry + 31) / 32);
     }
 }
 
@@ -523,7 +542,7 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
     const uint32_t nchunks = L.nblocks * L.cpb_total;
     hipLaunchKernelGGL(k_hist, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, hist);
     if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(64), 0, st, L, hist, binfo, ctab, ltab, hhdr,
+    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, hist, binfo, ctab, ltab, hhdr,
                        chunk_off, err);
     if (ev) (void)hipEventRecord(ev[1], st);
     hipLaunchKernelGGL(k_block_layout, dim3((L.nblocks + 63) / 64), dim3(64), 0, st, L.nblocks, binfo);

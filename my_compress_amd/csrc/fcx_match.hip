@@ -88,7 +88,7 @@ __device__ inline uint32_t lanes_below(uint64_t m) {
 // no bucket search ran): mbits of image position 0, written here per 64 positions.
 __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, uint16_t *step, uint32_t *s_red,
                                          uint32_t *s_unknown, uint32_t *mx, uint64_t *mbx, uint32_t q0, uint32_t npos,
-                                         uint32_t nload, uint32_t ilen, uint32_t w0) {
+                                         uint32_t nload, uint32_t ilen, uint32_t w0, uint32_t dbg) {
     const uint32_t tid = threadIdx.x;
     uint32_t *rbm = region + kTile / 2;                       // boundary bitmap, kRunBmWords
     uint16_t *prc = (uint16_t *)(rbm + kRunBmWords);          // prefix counts per bitmap word
@@ -117,6 +117,7 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
         }
     if (tid == 0) *s_unknown = 0;
     __syncthreads();
+    if (dbg & 8192u) return;   // timing: run table only
     // Evaluation, one chunk of 64 consecutive positions per wave step.  The chunk's
     // positions fall into a few own runs; for each, the wave scans the window's
     // runs one per lane, keeps those of the own run's byte (with ext, the run-level
@@ -137,70 +138,103 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
         const uint32_t kfirst = __shfl(ko, 0, 64), klast = __shfl(ko, 63, 64);
         uint32_t res = 0;
         bool lost = need && nruns > kRunTableCap;
-        for (uint32_t kr = kfirst; kr <= klast && nruns <= kRunTableCap; kr++) {
+        const bool table = nruns <= kRunTableCap;
+        // this lane's own run: r bytes left from xv, own run start / byte
+        const uint32_t own = table ? rt[ko] : 0u;
+        const uint32_t r = (table ? rt[ko + 1] & 0xFFFFu : xv) - xv;
+        const bool big = r > cap;
+        uint32_t best = 0;   // packed L << 13 | (8191 - j): max = longest, then leftmost
+        // The candidate lists of the chunk's own runs go side by side into the wave's list
+        // (as long as they fit) and are folded in one pass, each lane over its own run's
+        // list: the fold loop runs max(n) times instead of once per own run.
+        uint32_t lst = 0, ln = 0, used = 0;   // lane's pending list wl2[lst, lst + ln); used: wave-uniform
+        auto fold = [&](uint32_t base, uint32_t n) {
+            if (dbg & 32768u) n = 0;   // timing: no fold
+            // four entries per step, loaded unconditionally (clamped index) and folded by
+            // selects: no branch, so the four 8-B LDS reads are in flight together
+            for (uint32_t t = 0; t < n; t += 4) {
+                uint2 w[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) w[u] = wl2[base + min(t + u, n - 1)];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) {
+                    const uint32_t ep = w[u].x >> 16;
+                    const uint32_t sp = max(w[u].x & 0xFFFFu, xlo);
+                    const uint32_t A = ep - sp;
+                    const uint32_t Lr = min(r + w[u].y, cap);
+                    const bool ge = !big & (A >= r);
+                    const uint32_t Lc = ge ? Lr : min(A, cap);
+                    const uint32_t j = (ge & (w[u].y != 0) & (r < cap)) ? ep - r : sp;
+                    const uint32_t key = (Lc << 13) | (8191u - j);
+                    best = max(best, ((ep > xlo) & (t + u < n)) ? key : 0u);
+                }
+            }
+        };
+        auto flush = [&]() {   // fold the pending lists and free the list (wave-uniform call)
+            __builtin_amdgcn_wave_barrier();
+            fold(lst, ln);
+            ln = 0;
+            used = 0;
+            __builtin_amdgcn_wave_barrier();
+        };
+        // the window runs kc in [k0, min(k0 + 64, kr)) of the own run's byte, with ext
+        // (equal (byte, length) runs extend it; the first run that differs in length adds
+        // the shorter length and ends it; the query side meets the image end (sentinel)
+        // only past the cap), compacted into wl2 from `at`; returns their count
+        auto collect = [&](uint32_t k0, uint32_t kr, uint32_t cb, uint32_t vb0, uint32_t at) -> uint32_t {
+            const uint32_t kc = k0 + lane;
+            bool cand = false;
+            uint32_t se = 0, ext = 0;
+            if (kc < kr) {
+                const uint32_t v = rt[kc], nv = rt[kc + 1];
+                if ((v >> 16) == cb) {
+                    cand = true;
+                    se = (v & 0xFFFFu) | (nv << 16);
+                    uint32_t ka = kc + 1, kb = kr + 1, va = nv, vb = vb0;
+                    while ((va >> 16) == (vb >> 16)) {
+                        const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
+                        const uint32_t la = (na & 0xFFFFu) - (va & 0xFFFFu), lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
+                        if (la != lb) { ext += min(la, lb); break; }
+                        ext += la;
+                        if (ext >= kMaxL) break;
+                        ka++; kb++; va = na; vb = nb;
+                    }
+                }
+            }
+            const uint64_t cm = __ballot(cand);
+            if (cand) wl2[at + (uint32_t)__builtin_popcountll(cm & ((1ull << lane) - 1ull))] = make_uint2(se, ext);
+            return (uint32_t)__builtin_popcountll(cm);
+        };
+        for (uint32_t kr = kfirst; kr <= klast && table && !(dbg & 16384u); kr++) {
             const bool mine = need && ko == kr;
             const uint64_t in_run = __ballot(mine);
             if (in_run == 0ull) continue;
-            const uint32_t own = rt[kr], cb = own >> 16;
-            const uint32_t e = rt[kr + 1] & 0xFFFFu;
+            const uint32_t cb = rt[kr] >> 16;
             const uint32_t xf = c0 + (uint32_t)__builtin_ctzll(in_run);     // first position of the run here
             const uint32_t klo = run_rank(rbm, prc, max(w0 + xf, kWin) - kWin - w0) - 1;
             if (kr - klo > kRunBudget) { lost = lost || mine; continue; }
-            const uint32_t r = e - xv;
-            const bool big = r > cap;
-            uint32_t best = 0;   // packed L << 13 | (8191 - j): max = longest, then leftmost
             const uint32_t vb0 = rt[kr + 1];
-            for (uint32_t k0 = klo; k0 < kr; k0 += 64) {
-                const uint32_t kc = k0 + lane;
-                bool cand = false;
-                uint32_t se = 0, ext = 0;
-                if (kc < kr) {
-                    const uint32_t v = rt[kc], nv = rt[kc + 1];
-                    if ((v >> 16) == cb) {
-                        cand = true;
-                        se = (v & 0xFFFFu) | (nv << 16);
-                        // ext: equal (byte, length) runs extend it; the first run that
-                        // differs in length adds the shorter length and ends it.  The
-                        // query side meets the image end (sentinel) only past the cap.
-                        uint32_t ka = kc + 1, kb = kr + 1, va = nv, vb = vb0;
-                        while ((va >> 16) == (vb >> 16)) {
-                            const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
-                            const uint32_t la = (na & 0xFFFFu) - (va & 0xFFFFu), lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
-                            if (la != lb) { ext += min(la, lb); break; }
-                            ext += la;
-                            if (ext >= kMaxL) break;
-                            ka++; kb++; va = na; vb = nb;
-                        }
-                    }
+            if (kr - klo <= 64) {   // one pass of lanes over the window runs: a pending list
+                if (used + (kr - klo) > 64) flush();
+                const uint32_t n = collect(klo, kr, cb, vb0, used);
+                if (mine) { lst = used; ln = n; }
+                used += n;
+            } else {                // a long window: fold each pass of 64 runs at once
+                if (used) flush();
+                for (uint32_t k0 = klo; k0 < kr; k0 += 64) {
+                    const uint32_t n = collect(k0, kr, cb, vb0, 0);
+                    __builtin_amdgcn_wave_barrier();
+                    if (mine) fold(0, n);
+                    __builtin_amdgcn_wave_barrier();
                 }
-                const uint64_t cm = __ballot(cand);
-                if (cand) {
-                    const uint32_t slot = (uint32_t)__builtin_popcountll(cm & ((1ull << lane) - 1ull));
-                    wl2[slot] = make_uint2(se, ext);
-                }
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t n = (uint32_t)__builtin_popcountll(cm);
-                if (mine)
-                    for (uint32_t t = 0; t < n; t++) {   // branch-free candidate value
-                        const uint2 w = wl2[t];
-                        const uint32_t ep = w.x >> 16;
-                        const uint32_t sp = max(w.x & 0xFFFFu, xlo);
-                        const uint32_t A = ep - sp;
-                        const uint32_t Lr = min(r + w.y, cap);
-                        const bool ge = !big && A >= r;
-                        const uint32_t Lc = ge ? Lr : min(A, cap);
-                        const uint32_t j = (ge && w.y != 0 && r < cap) ? ep - r : sp;
-                        const uint32_t key = (Lc << 13) | (8191u - j);
-                        best = (ep > xlo && key > best) ? key : best;
-                    }
-                __builtin_amdgcn_wave_barrier();
             }
-            if (mine) {
-                const uint32_t sp = max(own & 0xFFFFu, xlo);
-                if (sp < xv) best = max(best, ((big ? cap : r) << 13) | (8191u - sp));
-                const uint32_t bL = best >> 13, bj = 8191u - (best & 0x1FFFu);
-                res = bL >= kMinL ? m_pack(bL, xv - bj) : 0u;
-            }
+        }
+        if (used) flush();
+        if (need && !lost) {
+            const uint32_t sp = max(own & 0xFFFFu, xlo);
+            if (sp < xv) best = max(best, ((big ? cap : r) << 13) | (8191u - sp));
+            const uint32_t bL = best >> 13, bj = 8191u - (best & 0x1FFFu);
+            res = bL >= kMinL ? m_pack(bL, xv - bj) : 0u;
         }
         if (mbx) {   // whole-tile mode: this wave writes the positions' mbits word and m row
             const uint64_t mb = __ballot(need && !lost && res != 0), lb = __ballot(lost);
@@ -776,7 +810,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     const bool dense = s_unknown != 0;   // matches may come from the run table: no fast path below
     if (dense)
         dense_phase(sdw, region, step, s_red, &s_unknown, m + bstart + w0,
-                    rmode ? mbits + (uint64_t)b * L.wpb + (w0 >> 6) : nullptr, q0, npos, nload, blen - w0, w0);
+                    rmode ? mbits + (uint64_t)b * L.wpb + (w0 >> 6) : nullptr, q0, npos, nload, blen - w0, w0, dbg);
 
     if (dbg & 64u) return;   // timing: + queries (no parse)
     uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
