@@ -298,9 +298,8 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
 
     if (ev) HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(hipMemsetAsync(c->dev_words, 0, 16, st));
-    HIP_TRY(hipMemsetAsync(c->s[0], 0, (uint64_t)L.sstride[0] * L.nblocks, st));
-    HIP_TRY(hipMemsetAsync(c->s[2], 0, (uint64_t)L.sstride[2] * L.nblocks, st));
-    HIP_TRY(hipMemsetAsync(c->s[3], 0, (uint64_t)L.sstride[3] * L.nblocks, st));
+    // (the flags / distance / golomb streams need no memset: k_stitch zeroes the words
+    // k_emit ORs into)
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
     launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok, st, c->match_mode);
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));

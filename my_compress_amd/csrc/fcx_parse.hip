@@ -267,11 +267,29 @@ __device__ inline void fetch_tile(const uint32_t *mt, const uint64_t *mb, const 
     cwv = lane < nw ? cw[lane] : 0ull;
 }
 
+// k_emit ORs each tile's two edge words of the flags, distance and golomb streams (the
+// words it shares with its neighbours); the stitch zeroes them at every tile boundary
+// (and the word after the block's last bit: the distance stream's (11 pCnt)/8 + 1 bytes
+// reach one byte past its bits), so the streams need no memset.  Lanes 8..13.
+__device__ inline void zero_edges(uint8_t *s_flags, uint8_t *s_p, uint8_t *s_golomb, const Layout &L, uint32_t b,
+                                  uint32_t tok, uint32_t mat, uint32_t gb) {
+    const uint32_t lane = lane_id();
+    if (lane < 8 || lane >= 14) return;
+    const uint32_t k = lane - 8, st = k >> 1;
+    const uint32_t pos = st == 0 ? tok : st == 1 ? kPBits * mat : gb;   // bit position of the boundary
+    if ((k & 1) == 0 && pos == 0) return;
+    const uint32_t wd = (k & 1) ? pos >> 5 : (pos - 1) >> 5;
+    uint8_t *base = st == 0 ? s_flags : st == 1 ? s_p : s_golomb;
+    ((uint32_t *)(base + (uint64_t)b * L.sstride[st == 0 ? 0 : st == 1 ? 2 : 3]))[wd] = 0u;
+}
+
 __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                                const uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain, const uint64_t *__restrict__ chain_pfx,
                                                const uint32_t *__restrict__ tinfo, const uint64_t *__restrict__ fp,
                                                const uint32_t *__restrict__ mtok, uint32_t *__restrict__ tile_off,
-                                               uint32_t *__restrict__ tconv, BlockInfo *__restrict__ binfo) {
+                                               uint32_t *__restrict__ tconv, BlockInfo *__restrict__ binfo,
+                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_p,
+                                               uint8_t *__restrict__ s_golomb) {
     __shared__ uint32_t mL[kTile];
     __shared__ uint32_t sti[64][6];          // per tile of the batch: flags, exit, totals, k_resolve verdict
     __shared__ uint32_t sfp[64][5];          // k_resolve: final counts, exit, conv record
@@ -325,6 +343,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         const uint32_t *mt = m + bstart + t0;
         const uint32_t nw = (t1 - t0 + 63) / 64;
         if (lane < 3) tile_off[3 * tix + lane] = lane == 0 ? run.tok : lane == 1 ? run.mat : run.gb;
+        zero_edges(s_flags, s_p, s_golomb, L, b, run.tok, run.mat, run.gb);
         if (e >= t1) {  // a match spans the whole tile
             for (uint32_t w = lane; w < nw; w += 64) cw[w] = 0;
             if (lane == 0) tconv[tix] = kConvAll;
@@ -448,6 +467,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         run.tok += walked.tok; run.mat += walked.mat; run.gb += walked.gb;
         e = exitv;
     }
+    zero_edges(s_flags, s_p, s_golomb, L, b, run.tok, run.mat, run.gb);
     if (lane == 0) {
         BlockInfo &bi = binfo[b];
         bi.len = blen;
@@ -777,7 +797,7 @@ void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_
     const uint32_t ntiles = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_resolve, dim3(ntiles), dim3(64), 0, st, L, m, mbits, chain, chain_pfx, tinfo, fp);
     hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, mtok,
-                       tile_off, tconv, binfo);
+                       tile_off, tconv, binfo, s_flags, s_p, s_golomb);
     if (ev) (void)hipEventRecord(ev[0], st);
     hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok, tconv,
                        tinfo, s_flags, s_chars, s_p, s_golomb);

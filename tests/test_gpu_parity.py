@@ -115,6 +115,8 @@ def test_dense_and_periodic_edges(gpu_compress):
         inputs.generate("runs", 77, 300000),
         bytes(range(256)) * 300,
         b"a" * 4097 + b"b" * 4095 + b"a" * 4096,
+        # uniform tiles (one byte value over the whole window: m_uniform) between others
+        b"\x07" * 20000 + inputs.generate("text", 5, 30000) + b"\xff" * 9000 + b"\x07" * 70000,
     ]
     for data in cases:
         for block in [4096, 65536, 1 << 20]:
