@@ -128,17 +128,18 @@ __global__ __launch_bounds__(kEncT) void k_hist(Layout L, const BlockInfo *__res
 }
 
 // ---------------------------------------------------------------------------
-constexpr uint32_t kTreeT = 256;   // k_tree workgroup: one thread per symbol / per chunk
+constexpr uint32_t kTreeT = 128;   // k_tree workgroup: two waves (more trees per CU: the merge is serial)
+constexpr uint32_t kTreeW = kTreeT / 64;
 
 __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__restrict__ hist,
                                                  BlockInfo *__restrict__ binfo, uint32_t *__restrict__ ctab,
                                                  uint8_t *__restrict__ ltab, uint8_t *__restrict__ hhdr,
                                                  uint32_t *__restrict__ chunk_off, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint32_t w[256];
-    __shared__ uint32_t sw[256], ss[256], ln[256];
+    __shared__ uint32_t sw[257], ss[257], ln[256];   // (the merge reads the leaf queue two deep)
     __shared__ uint32_t iw[256], il[256], ir[256], par[512];
-    __shared__ uint32_t part[4][256];
-    __shared__ uint32_t s_red[4];
+    __shared__ uint32_t part[kTreeW][256];
+    __shared__ uint32_t s_red[kTreeW];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / kStreams, s = blockIdx.x % kStreams;
     BlockInfo &bi = binfo[b];
@@ -151,57 +152,79 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__res
     for (uint32_t q = 0; q < s; q++) r0 += L.cpb[q];
     const uint32_t nch = (bi.slen[s] + kChunk - 1) / kChunk;
     const uint32_t *hc = hist + ((uint64_t)b * L.cpb_total + r0) * 256;   // this stream's chunk histograms
-    {   // symbol weights: wave wv sums the chunks c = wv mod 4 (lane: symbols lane + 64 q)
+    {   // symbol weights: wave wv sums the chunks c = wv mod kTreeW (lane: symbols lane + 64 q)
         uint32_t acc[4] = {0, 0, 0, 0};
 #pragma unroll 8
-        for (uint32_t c = wv; c < nch; c += 4)
+        for (uint32_t c = wv; c < nch; c += kTreeW)
 #pragma unroll
             for (uint32_t q = 0; q < 4; q++) acc[q] += hc[c * 256 + lane + 64 * q];
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) part[wv][lane + 64 * q] = acc[q];
     }
     __syncthreads();
-    const uint32_t wt = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
-    w[tid] = wt;
-    const uint32_t real = (uint32_t)__syncthreads_count(wt != 0);
-    // stable sort of the leaves by (weight, symbol): rank = number of smaller keys
-    if (wt) {
-        const uint64_t key = ((uint64_t)wt << 8) | tid;
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < 256; j += 4) {
-            const uint4 w4 = *(const uint4 *)&w[j];
-            const uint32_t wj[4] = {w4.x, w4.y, w4.z, w4.w};
+    uint32_t nz = 0;
 #pragma unroll
-            for (uint32_t u = 0; u < 4; u++)
-                rank += (wj[u] != 0 && (((uint64_t)wj[u] << 8) | (j + u)) < key) ? 1u : 0u;
+    for (uint32_t u = 0; u < 256 / kTreeT; u++) {
+        const uint32_t sym = tid + kTreeT * u;
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kTreeW; q++) t += part[q][sym];
+        w[sym] = t;
+        nz += t != 0 ? 1u : 0u;
+    }
+    const uint32_t real = (uint32_t)__syncthreads_count(nz >= 1) + (uint32_t)__syncthreads_count(nz >= 2);
+    // stable sort of the leaves by (weight, symbol): rank = number of smaller keys
+#pragma unroll
+    for (uint32_t u = 0; u < 256 / kTreeT; u++) {
+        const uint32_t sym = tid + kTreeT * u, wt = w[sym];
+        if (wt) {
+            const uint64_t key = ((uint64_t)wt << 8) | sym;
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < 256; j += 4) {
+                const uint4 w4 = *(const uint4 *)&w[j];
+                const uint32_t wj[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                for (uint32_t v = 0; v < 4; v++)
+                    rank += (wj[v] != 0 && (((uint64_t)wj[v] << 8) | (j + v)) < key) ? 1u : 0u;
+            }
+            sw[rank] = wt;
+            ss[rank] = sym;
         }
-        sw[rank] = wt;
-        ss[rank] = tid;
     }
     __syncthreads();
     const uint32_t nint = real >= 2 ? real - 1 : 0;
     if (tid == 0 && nint) {
-        // two-queue merge == the reference's sorted-list re-insertion (570-611)
+        // two-queue merge == the reference's sorted-list re-insertion (570-611).  Each step
+        // reads both queue heads two deep at once (one LDS round trip per step)
         uint32_t lq = 0, iq = 0;
         for (uint32_t kk = 0; kk < nint; kk++) {
-            uint32_t id[2], wq[2];
-            for (int h = 0; h < 2; h++) {
-                if (lq < real && (iq >= kk || sw[lq] <= iw[iq])) { id[h] = ss[lq]; wq[h] = sw[lq]; lq++; }
-                else { id[h] = 256 + iq; wq[h] = iw[iq]; iq++; }
+            const uint32_t L0 = sw[lq], L1 = sw[lq + 1], S0 = ss[lq], S1 = ss[lq + 1];
+            const uint32_t I0 = iw[iq], I1 = iw[iq + 1];
+            uint32_t id0, w0, id1, w1;
+            if (lq < real && (iq >= kk || L0 <= I0)) {   // first: leaf
+                id0 = S0; w0 = L0;
+                if (lq + 1 < real && (iq >= kk || L1 <= I0)) { id1 = S1; w1 = L1; lq += 2; }
+                else { id1 = 256 + iq; w1 = I0; lq += 1; iq += 1; }
+            } else {                                      // first: internal node
+                id0 = 256 + iq; w0 = I0;
+                if (lq < real && (iq + 1 >= kk || L0 <= I1)) { id1 = S0; w1 = L0; lq += 1; iq += 1; }
+                else { id1 = 256 + iq + 1; w1 = I1; iq += 2; }
             }
-            iw[kk] = wq[0] + wq[1];
-            il[kk] = id[0];
-            ir[kk] = id[1];
-            par[id[0]] = 256 + kk;
-            par[id[1]] = 256 + kk;
+            iw[kk] = w0 + w1;
+            il[kk] = id0;
+            ir[kk] = id1;
+            par[id0] = 256 + kk;
+            par[id1] = 256 + kk;
         }
     }
     __syncthreads();
     const uint32_t root = 256 + nint - 1;
-    {   // code of symbol tid: root -> leaf path, root decision in bit 0
+#pragma unroll
+    for (uint32_t u = 0; u < 256 / kTreeT; u++) {   // code of a symbol: root -> leaf path, root decision in bit 0
+        const uint32_t sym = tid + kTreeT * u;
         uint32_t code = 0, len = 0;
-        if (nint && wt) {
-            uint32_t cur = tid;
+        if (nint && w[sym]) {
+            uint32_t cur = sym;
             while (cur != root && len <= 32) {
                 const uint32_t p = par[cur];
                 code = (code << 1) | (ir[p - 256] == cur ? 1u : 0u);
@@ -210,9 +233,9 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__res
             }
             if (len > 32) atomicOr(err, kErrCodeLen);
         }
-        ctab[hb + tid] = code;
-        ltab[hb + tid] = (uint8_t)len;
-        ln[tid] = len;
+        ctab[hb + sym] = code;
+        ltab[hb + sym] = (uint8_t)len;
+        ln[sym] = len;
     }
     __syncthreads();
     // starting bit of every chunk: chunk histogram . code lengths (thread c: chunk c, its
@@ -233,7 +256,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__res
         if (lane == 63) s_red[wv] = inc;
         __syncthreads();
         uint32_t pre = 0, all = 0;
-        for (uint32_t q = 0; q < 4; q++) {
+        for (uint32_t q = 0; q < kTreeW; q++) {
             if (q < wv) pre += s_red[q];
             all += s_red[q];
         }
