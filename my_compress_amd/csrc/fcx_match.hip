@@ -477,7 +477,9 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     uint16_t *ent = (uint16_t *)(region + kHeadWords);     // window entries, bucket-sorted
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
-    __shared__ uint32_t s_nruns;
+    __shared__ uint32_t s_nruns;    // image runs counted in the first 2 KiB (pass 1)
+    __shared__ uint32_t s_nruns2;   // ... and in the rest (pass 2, only when pass 1 allows run mode)
+    __shared__ uint32_t s_smp[kSampleWords];   // repeat sample bitmap
     __shared__ uint32_t s_sample;   // repeat sample: sampled keys whose hash was seen before
     __shared__ uint32_t s_events;   // repeat filter: window keys whose hash was seen before
     __shared__ uint32_t s_np;       // sparse search: positions whose hash repeats
@@ -525,8 +527,15 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             sdw[x] = v;
         }
     }
-    if (tid == 0) { s_unknown = 0; s_match = 0; s_nruns = 0; s_sample = 0; s_chg[0] = 0; s_chg[1] = 0; }
-    if (tid < kSampleWords) region[tid] = 0;
+    if (tid == 0) {
+        s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_sample = 0; s_chg[0] = 0; s_chg[1] = 0;
+        s_events = 0; s_np = 0;
+    }
+    if (tid < kSampleWords) s_smp[tid] = 0;
+    {   // the repeat filter's bitmaps are zeroed here, under the staging loads' latency
+        uint4 *r4 = (uint4 *)region;
+        for (uint32_t x = tid; x < kFilterWords / 4; x += kMT) r4[x] = make_uint4(0u, 0u, 0u, 0u);
+    }
     __syncthreads();
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
@@ -558,21 +567,22 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             if (x + 3 <= nload) {
                 const uint32_t hs = key_mix(lds_key3(sdw, x)) >> 12;
                 const uint32_t bit = 1u << (hs & 31);
-                rep = (atomicOr(&region[hs >> 5], bit) & bit) != 0;
+                rep = (atomicOr(&s_smp[hs >> 5], bit) & bit) != 0;
             }
             const uint64_t bal = __ballot(rep);
             if ((tid & 63) == 0 && bal) atomicAdd(&s_sample, (uint32_t)__popcll(bal));
         }
         __syncthreads();
-        if (s_nruns <= kRunTile) {
+        if (s_nruns <= kRunTile) {   // (s_nruns is final here: the decision is uniform)
             cnt = 0;
             for (uint32_t w = tid + kMT; 4 * w < nload; w += kMT) cnt += runs_in(w);
             cnt = wave_sum_u32(cnt);
-            if ((tid & 63) == 0 && cnt) atomicAdd(&s_nruns, cnt);
+            if ((tid & 63) == 0 && cnt) atomicAdd(&s_nruns2, cnt);
+            __syncthreads();
         }
     }
-    __syncthreads();
-    const bool rmode = (s_nruns <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
+    const uint32_t nruns_img = s_nruns + s_nruns2;   // s_nruns2 = 0 unless pass 2 ran (then after its barrier)
+    const bool rmode = (nruns_img <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
     if (dbg & 16u) return;   // timing: staging + run count only
 
     // this lane's 12 consecutive window positions 12 tid .. 12 tid + 11 take their keys from
@@ -587,7 +597,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     };
 
     if (rmode) {
-        if (s_nruns == 1 && !(dbg & 12u)) {   // one byte value over the whole image (zeros)
+        if (nruns_img == 1 && !(dbg & 12u)) {   // one byte value over the whole image (zeros)
             uniform_tile_out(region, s_red, mbits + (uint64_t)b * L.wpb,
                              chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64),
                              chain_pfx + (uint64_t)blockIdx.x * (kTile / 64), tinfo + 8ull * blockIdx.x, t0, t1, blen);
@@ -604,13 +614,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // (sparse search); above kSparseEvents repeats the tile takes the bucket search. ----
     bool sparse = false;
     if (s_sample <= kSampleEvents && !(dbg & 128u)) {
-    uint32_t *seen = region, *dupm = region + kFilterWords / 2;
-    {
-        uint4 *r4 = (uint4 *)region;
-        for (uint32_t x = tid; x < kFilterWords / 4; x += kMT) r4[x] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    if (tid == 0) { s_events = 0; s_np = 0; }
-    __syncthreads();
+    uint32_t *seen = region, *dupm = region + kFilterWords / 2;   // (zeroed with the staging)
     {
         // all 12 "seen" atomics in flight at once (program order keeps a lane's own
         // repeats visible to it), then the "dup" marks without return values
