@@ -283,6 +283,19 @@ __device__ inline void zero_edges(uint8_t *s_flags, uint8_t *s_p, uint8_t *s_gol
     ((uint32_t *)(base + (uint64_t)b * L.sstride[st == 0 ? 0 : st == 1 ? 2 : 3]))[wd] = 0u;
 }
 
+// the same six words, all from the calling lane (the batched fast path: one lane per tile)
+__device__ inline void zero_edges_lane(uint8_t *s_flags, uint8_t *s_p, uint8_t *s_golomb, const Layout &L, uint32_t b,
+                                       uint32_t tok, uint32_t mat, uint32_t gb) {
+#pragma unroll
+    for (uint32_t st = 0; st < 3; st++) {
+        const uint32_t pos = st == 0 ? tok : st == 1 ? kPBits * mat : gb;
+        uint32_t *w = (uint32_t *)((st == 0 ? s_flags : st == 1 ? s_p : s_golomb) +
+                                   (uint64_t)b * L.sstride[st == 0 ? 0 : st == 1 ? 2 : 3]);
+        if (pos) w[(pos - 1) >> 5] = 0u;
+        w[pos >> 5] = 0u;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                                const uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain, const uint64_t *__restrict__ chain_pfx,
                                                const uint32_t *__restrict__ tinfo, const uint64_t *__restrict__ fp,
@@ -333,6 +346,44 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 }
             }
             __syncthreads();
+        }
+        {   // batched fast path: the leading tiles of the batch whose k_resolve record applies
+            // (each one's assumed entry is its predecessor's recorded exit, starting from e)
+            // are committed at once, one lane per tile, counts by a wave prefix sum
+            const uint32_t u = lane, jj = j + u, kk = k + u;
+            bool ok = jj < 64 && kk < ntiles;
+            uint32_t ct = 0, cm = 0, cg = 0;
+            if (ok) {
+                const uint32_t t0u = kk * kTile, t1u = min(blen, t0u + kTile);
+                const uint32_t eu = u == 0 ? e : sfp[jj - 1][3];
+                const uint32_t fpv = sti[jj][5];
+                ok = (sti[jj][0] & kTileUniform) == 0 && (fpv & 1u) && eu >= t0u && eu < t1u &&
+                     eu - t0u == ((fpv >> 1) & 0x7FFFu);
+            }
+            const uint64_t okm = __ballot(ok);
+            const uint32_t F = ~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u;   // leading committed tiles
+            if (F >= 2) {
+                if (u < F) { ct = sfp[jj][0]; cm = sfp[jj][1]; cg = sfp[jj][2]; }
+                const uint32_t it = wave_incl_scan(ct), im = wave_incl_scan(cm), ig = wave_incl_scan(cg);
+                if (u < F) {
+                    const uint32_t tixu = tix + u;
+                    const uint32_t pt = run.tok + it - ct, pm = run.mat + im - cm, pg = run.gb + ig - cg;
+                    tile_off[3 * tixu + 0] = pt;
+                    tile_off[3 * tixu + 1] = pm;
+                    tile_off[3 * tixu + 2] = pg;
+                    zero_edges_lane(s_flags, s_p, s_golomb, L, b, pt, pm, pg);
+                    const uint32_t fpv = sti[jj][5], nmod = fpv >> 16;
+                    uint64_t *cwu = chain + (uint64_t)b * L.wpb + (uint64_t)kk * (kTile / 64);
+                    for (uint32_t w = 0; w < nmod; w++) cwu[w] = sfw[jj][w];
+                    tconv[tixu] = (sti[jj][0] & kTileMFull) ? kConvAll : sfp[jj][4];
+                }
+                run.tok += (uint32_t)__builtin_amdgcn_readlane((int)it, (int)(F - 1));
+                run.mat += (uint32_t)__builtin_amdgcn_readlane((int)im, (int)(F - 1));
+                run.gb += (uint32_t)__builtin_amdgcn_readlane((int)ig, (int)(F - 1));
+                e = sfp[j + F - 1][3];
+                k += F - 1;
+                continue;
+            }
         }
         const bool lazy = (sti[j][0] & kTileLazy) != 0;
         const bool mfull = (sti[j][0] & kTileMFull) != 0;   // else m[] rows stop at kResolveSpan
