@@ -385,6 +385,51 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 continue;
             }
         }
+        {   // batched uniform tiles: where every token is 258 long (one byte value, no block
+            // start, >= 258 bytes to the block end) the chain from e is e + 258 m, so the
+            // leading such tiles of the batch are committed at once in closed form
+            constexpr uint32_t kStep = kMaxL;                 // L = 257, cursor += 258
+            constexpr uint32_t kGb = ((kMaxL - 1) >> 2) + 3;  // golomb bits of one such token
+            const uint32_t u = lane, jj = j + u, kk = k + u;
+            const uint32_t t0u = kk * kTile, t1u = min(blen, t0u + kTile);
+            const bool ok = jj < 64 && kk < ntiles && (sti[jj][0] & kTileUniform) && t0u >= 1 && t1u + kMaxL - 1 <= blen &&
+                            e >= t0 && e < t1;
+            const uint64_t okm = __ballot(ok);
+            const uint32_t F = ~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u;
+            if (F >= 2) {
+                uint32_t nt = 0, eu = 0;
+                if (u < F) {
+                    eu = u == 0 ? e : e + kStep * ((t0u - e + kStep - 1) / kStep);   // first chain position >= t0u
+                    nt = (t1u - eu + kStep - 1) / kStep;
+                }
+                const uint32_t it = wave_incl_scan(nt);
+                if (u < F) {
+                    const uint32_t tixu = tix + u;
+                    const uint32_t pt = run.tok + it - nt, pm = run.mat + it - nt, pg = run.gb + kGb * (it - nt);
+                    tile_off[3 * tixu + 0] = pt;
+                    tile_off[3 * tixu + 1] = pm;
+                    tile_off[3 * tixu + 2] = pg;
+                    zero_edges_lane(s_flags, s_p, s_golomb, L, b, pt, pm, pg);
+                    uint64_t *cwu = chain + (uint64_t)b * L.wpb + (uint64_t)kk * (kTile / 64);
+                    const uint32_t nwu = (t1u - t0u + 63) / 64;
+                    for (uint32_t w = 0; w < nwu; w++) {
+                        const uint32_t lo = t0u + 64 * w;
+                        const uint32_t p = lo <= eu ? eu : eu + kStep * ((lo - eu + kStep - 1) / kStep);
+                        cwu[w] = p < min(lo + 64, t1u) ? 1ull << (p - lo) : 0ull;
+                    }
+                    tconv[tixu] = kConvAll;
+                }
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)it, (int)(F - 1));
+                run.tok += tot;
+                run.mat += tot;
+                run.gb += kGb * tot;
+                const uint32_t eF = (uint32_t)__builtin_amdgcn_readlane((int)eu, (int)(F - 1)),
+                               nF = (uint32_t)__builtin_amdgcn_readlane((int)nt, (int)(F - 1));
+                e = eF + kStep * nF;
+                k += F - 1;
+                continue;
+            }
+        }
         const bool lazy = (sti[j][0] & kTileLazy) != 0;
         const bool mfull = (sti[j][0] & kTileMFull) != 0;   // else m[] rows stop at kResolveSpan
         const bool uni = (sti[j][0] & kTileUniform) != 0;  // m = m_uniform, no rows
