@@ -12,8 +12,11 @@
 //      bijection of Z/2^24 gives a 13-bit bucket; 16-bit entries keep the position
 //      and 3 more hash bits, the rare collisions are rejected by comparing key
 //      bytes); a bucket is one contiguous LDS range (16-bit counters by LDS
-//      atomics, block scan, scatter);
-//   3. every tile position scans its bucket range (independent LDS loads, no
+//      atomics, block scan, scatter), its entries in slab order (12 barrier-
+//      separated insertion passes of 512 positions), and the bucket counters
+//      sampled during the passes bound each query's window [x - 2047, x) inside
+//      its bucket;
+//   3. every tile position scans that part of its bucket (independent LDS loads, no
 //      pointer chase; four queries interleaved per lane) and keeps the
 //      max-length / min-position candidate among entries in its window (stored
 //      to m[] only where a match or "unknown" results, flagged per position in
@@ -655,23 +658,50 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __syncthreads();
 
     // ---- 2. counting sort of the window positions by bucket ----
-    // 16-bit counters, two per dword (a bucket never exceeds 6144 entries)
+    // 16-bit counters, two per dword (a bucket never exceeds 6144 entries).  Pass p inserts
+    // the slab [512 p, 512 p + 512) of window positions (x = tid + kMT p), one barrier per
+    // pass, so a bucket lists its entries slab by slab in position order.  A query at x
+    // (slab s = x / 512) needs only the entries in [x - 2047, x): slabs s - 4 .. s.  Its
+    // bucket counter read during pass s - 5 (before that pass's barrier: every slab <= s - 6
+    // is in, slab s - 5 partly) bounds from below the entries left of slab s - 4 (all out of
+    // the window); read during pass s + 1 (after the barrier of pass s) it bounds from above
+    // the entries of slabs <= s (every later entry lies right of x).  The query scans only
+    // between the two snapshots: about half of its bucket.
     uint32_t ins_hr[kIns];                                             // bucket << 16 | tag << 13 | rank
+    uint32_t snap[kQPL];   // query r: lo rank | hi rank << 16 (hi 0xFFFF = bucket end)
+    const uint32_t qsl = q0 >> 9;   // slab of query r = r + qsl (q0 = 0 or 2048)
 #pragma unroll
-    for (uint32_t r = 0; r < kIns; r++) {
-        ins_hr[r] = 0xFFFFFFFFu;
-        // position-strided (x = tid + kMT r): ranks within a bucket come out roughly in
-        // position order, so a query meets its leftmost candidates first (fewer long
-        // extensions survive the right-of-best pruning); measured faster than keys from
-        // the lane's registers on text and dna
-        if (tid + kMT * r < ins_end) {
-            const uint32_t h = key_mix(lds_key3(sdw, tid + kMT * r));
+    for (uint32_t r = 0; r < kQPL; r++) snap[r] = 0xFFFF0000u;
+    auto qbucket = [&](uint32_t r) -> uint32_t {   // bucket of query r (its insertion record)
+        return (qsl ? ins_hr[r + 4] : ins_hr[r]) >> 16;
+    };
+    auto counter = [&](uint32_t bk) -> uint32_t { return (hw[bk >> 1] >> (16 * (bk & 1))) & 0xFFFFu; };
+#pragma unroll
+    for (uint32_t p = 0; p < kIns; p++) {
+        ins_hr[p] = 0xFFFFFFFFu;
+        if (tid + kMT * p < ins_end) {
+            const uint32_t h = key_mix(lds_key3(sdw, tid + kMT * p));
             const uint32_t bk = h >> (24 - kHashBits), sh = 16 * (bk & 1);
             const uint32_t old = atomicAdd(&hw[bk >> 1], 1u << sh);
-            ins_hr[r] = (bk << 16) | ((h & 7u) << 13) | ((old >> sh) & 0x1FFFu);   // rank < 6144
+            ins_hr[p] = (bk << 16) | ((h & 7u) << 13) | ((old >> sh) & 0x1FFFu);   // rank < 6144
         }
+        // snapshots taken in pass p: lo of the query whose slab is p + 5, hi of the query
+        // whose slab is p - 1 (queries of slabs qsl .. qsl + 7; unsearched queries have no
+        // insertion record and keep the whole bucket, unused)
+#pragma unroll
+        for (uint32_t r = 0; r < kQPL; r++) {
+            // lo: the query is not inserted yet; its bucket comes from its key
+            if ((qsl == 4 && p + 1 == r) || (qsl == 0 && p + 5 == r)) {
+                const uint32_t bk = key_mix(lds_key3(sdw, q0 + tid + kMT * r)) >> (24 - kHashBits);
+                snap[r] = (snap[r] & 0xFFFF0000u) | counter(bk);
+            }
+            if ((qsl == 4 && p == r + 5) || (qsl == 0 && p == r + 1)) {
+                const uint32_t bk = qbucket(r);
+                if (bk != 0xFFFFu) snap[r] = (snap[r] & 0xFFFFu) | (counter(bk) << 16);
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
     {   // exclusive scan of the bucket counts: kBkDw consecutive counter dwords per lane
         constexpr uint32_t kBkDw = (1u << kHashBits) / 2 / kMT;
         uint32_t cw4[kBkDw], sum = 0;
@@ -723,7 +753,9 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     qc[u] = lds_ld4(sdw, x + 8);
                     const uint32_t h = key_mix(qa[u] & 0xFFFFFFu);
                     const uint32_t bk = h >> (24 - kHashBits);
-                    const uint32_t lo = h16[bk], n = h16[bk + 1] - lo;
+                    const uint32_t b0 = h16[bk], b1 = h16[bk + 1], sn = snap[g + u];
+                    const uint32_t lo = b0 + (sn & 0xFFFFu);
+                    const uint32_t n = ((sn >> 16) == 0xFFFFu ? b1 : min(b1, b0 + (sn >> 16))) - lo;
                     xpk[u] = x | (cap << 13) | ((h & 7u) << 22);   // bits 25..31: extension count
                     if (n > kMaxChainSteps) rng[u] = 0xFFFFFFFFu;
                     else { rng[u] = lo | (n << 16); nmax = max(nmax, n); }
