@@ -668,10 +668,15 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // the entries of slabs <= s (every later entry lies right of x).  The query scans only
     // between the two snapshots: about half of its bucket.
     uint32_t ins_hr[kIns];                                             // bucket << 16 | tag << 13 | rank
-    uint32_t snap[kQPL];   // query r: lo rank | hi rank << 16 (hi 0xFFFF = bucket end)
+    // queries 0..3: lo rank | hi rank << 16 (hi 0xFFFF = bucket end); queries 4..7 (live
+    // through the first group's search: two registers) keep only their lo rank, the bound
+    // that prunes most there, two u16 per register
+    uint32_t snap[kQPL / 2], slo[kQPL / 4];
     const uint32_t qsl = q0 >> 9;   // slab of query r = r + qsl (q0 = 0 or 2048)
 #pragma unroll
-    for (uint32_t r = 0; r < kQPL; r++) snap[r] = 0xFFFF0000u;
+    for (uint32_t r = 0; r < kQPL / 2; r++) snap[r] = 0xFFFF0000u;
+#pragma unroll
+    for (uint32_t r = 0; r < kQPL / 4; r++) slo[r] = 0u;
     auto qbucket = [&](uint32_t r) -> uint32_t {   // bucket of query r (its insertion record)
         return (qsl ? ins_hr[r + 4] : ins_hr[r]) >> 16;
     };
@@ -693,11 +698,12 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             // lo: the query is not inserted yet; its bucket comes from its key
             if ((qsl == 4 && p + 1 == r) || (qsl == 0 && p + 5 == r)) {
                 const uint32_t bk = key_mix(lds_key3(sdw, q0 + tid + kMT * r)) >> (24 - kHashBits);
-                snap[r] = (snap[r] & 0xFFFF0000u) | counter(bk);
+                if (r < kQPL / 2) snap[r % (kQPL / 2)] = (snap[r % (kQPL / 2)] & 0xFFFF0000u) | counter(bk);
+                else slo[(r - kQPL / 2) >> 1] |= counter(bk) << (16 * (r & 1));
             }
-            if ((qsl == 4 && p == r + 5) || (qsl == 0 && p == r + 1)) {
+            if (r < kQPL / 2 && ((qsl == 4 && p == r + 5) || (qsl == 0 && p == r + 1))) {
                 const uint32_t bk = qbucket(r);
-                if (bk != 0xFFFFu) snap[r] = (snap[r] & 0xFFFFu) | (counter(bk) << 16);
+                if (bk != 0xFFFFu) snap[r % (kQPL / 2)] = (snap[r % (kQPL / 2)] & 0xFFFFu) | (counter(bk) << 16);
             }
         }
         __syncthreads();
@@ -753,7 +759,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     qc[u] = lds_ld4(sdw, x + 8);
                     const uint32_t h = key_mix(qa[u] & 0xFFFFFFu);
                     const uint32_t bk = h >> (24 - kHashBits);
-                    const uint32_t b0 = h16[bk], b1 = h16[bk + 1], sn = snap[g + u];
+                    const uint32_t sn = g == 0 ? snap[u] : 0xFFFF0000u | ((slo[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+                    const uint32_t b0 = h16[bk], b1 = h16[bk + 1];
                     const uint32_t lo = b0 + (sn & 0xFFFFu);
                     const uint32_t n = ((sn >> 16) == 0xFFFFu ? b1 : min(b1, b0 + (sn >> 16))) - lo;
                     xpk[u] = x | (cap << 13) | ((h & 7u) << 22);   // bits 25..31: extension count
