@@ -734,6 +734,61 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         else
             for (uint32_t j = 0; j < 4 && xa + j < blen; j++) la |= (uint32_t)d[xa + j] << (8 * j);
     }
+    if (uni) {
+        // one byte value over the tile and its window (zeros): a token's m is m_uniform, its
+        // char the tile's byte (at i + L, inside the uniform window); no input staging, no
+        // m rows, no match list, just the few tokens' bits
+        uint32_t bits = 0;
+        if (s < t1) {
+            bits = (uint32_t)(cwv >> (16 * (tid & 3))) & 0xFFFFu;
+            if (t1 - s < 16) bits &= (1u << (t1 - s)) - 1u;
+        }
+        const uint8_t ub = (uint8_t)in4[0];   // (lanes with tokens lie inside the tile)
+        uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0}, tot[3];
+        for (uint32_t bb = bits; bb; bb &= bb - 1) {
+            const uint32_t Lm = m_len(m_uniform(s + __builtin_ctz(bb), blen));
+            if (Lm) { v[1]++; v[2] += (Lm >> 2) + 3; }
+        }
+        for (uint32_t w = tid; w < kFlagW; w += 256) lf[w] = 0;
+        for (uint32_t w = tid; w < kPW; w += 256) lp[w] = 0;
+        for (uint32_t w = tid; w < kGW; w += 256) lg[w] = 0;
+        block_scan3(v, tot, sh);   // (its barriers also order the zeroing before the ORs)
+        const uint32_t fw0 = tok0 >> 5, pw0 = (uint32_t)(((uint64_t)kPBits * mi0) >> 5), gw0 = g0 >> 5;
+        uint8_t *chars = s_chars + (uint64_t)b * L.sstride[1];
+        uint32_t fl = 0, nt_lane = 0, np_lane = 0, goff = g0 + v[2];
+        uint64_t pacc = 0;
+        for (uint32_t bb = bits; bb; bb &= bb - 1) {
+            const uint32_t mu = m_uniform(s + __builtin_ctz(bb), blen), Lm = m_len(mu);
+            chars[tok0 + v[0] + nt_lane] = ub;
+            if (Lm == 0) {
+                fl |= 1u << nt_lane;
+            } else {
+                pacc |= (uint64_t)m_dist(mu) << (kPBits * np_lane);
+                np_lane++;
+                const uint32_t qq = Lm >> 2, r = Lm & 3;   // q one-bits, a zero bit, r (2 bits)
+                uint32_t pos = goff, left = qq;
+                while (left) {
+                    const uint32_t sh_ = pos & 31, n = min(left, 32 - sh_);
+                    atomicOr(&lg[(pos >> 5) - gw0], (n == 32 ? ~0u : ((1u << n) - 1)) << sh_);
+                    pos += n;
+                    left -= n;
+                }
+                if (r) or_bits64(lg, gw0, pos + 1, r, 2);
+                goff += qq + 3;
+            }
+            nt_lane++;
+        }
+        or_bits64(lf, fw0, tok0 + v[0], fl, nt_lane);
+        or_bits64(lp, pw0, (uint64_t)kPBits * (mi0 + v[1]), pacc, kPBits * np_lane);
+        __syncthreads();
+        const uint32_t nfw = tot[0] ? ((tok0 + tot[0] - 1) >> 5) - fw0 + 1 : 0;
+        const uint32_t npw = tot[1] ? (uint32_t)(((uint64_t)kPBits * (mi0 + tot[1]) - 1) >> 5) - pw0 + 1 : 0;
+        const uint32_t ngw = tot[2] ? ((g0 + tot[2] - 1) >> 5) - gw0 + 1 : 0;
+        flush_words((uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]), fw0, lf, nfw, tid);
+        flush_words((uint32_t *)(s_p + (uint64_t)b * L.sstride[2]), pw0, lp, npw, tid);
+        flush_words((uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]), gw0, lg, ngw, tid);
+        return;
+    }
 #pragma unroll
     for (uint32_t q = 0; q < 4; q++) lin[4 * tid + q] = in4[q];
     if (tid < kInW - kTile / 4) lin[kTile / 4 + tid] = la;
