@@ -572,9 +572,55 @@ __global__ __launch_bounds__(kDSymThreads) void k_dsyms(const uint8_t *in, uint6
         for (uint32_t x = tid; x < (1u << kDTblBits); x += kDSymThreads) T[x] = tbl[(1ull << kDTblBits) * q + x];
         for (uint32_t x = tid; x < 2 * s.ts; x += kDSymThreads) C[x] = child[512ull * q + x];
         __syncthreads();
-        uint64_t bit0;
-        const BitBuf src = make_bits(in, in_len, bit0);
-        got = seg_decode<false>(src, bit0 + s.words_bit, s.nbits, s.count, T, C, dst, nullptr, st, cnt, flag, stats);
+        // every code 8 bits long (a complete depth-8 tree: the chars of random data): the
+        // codes are the stream's bytes (the words start on a byte), so symbol i is T[byte i]
+        // - a byte substitution, 16 bytes per lane and step, no segment agreement
+        static_assert(kDSymThreads == (1u << kDTblBits), "one table entry per lane");
+        const uint32_t e = T[tid];
+        if (__syncthreads_and(!(e & 0x8000u) && ((e >> 8) & 0x1Fu) == 8u)) {
+            got = min(s.count, s.nbits / 8);
+            const uintptr_t a = (uintptr_t)(in + (s.words_bit >> 3)), aw = a & ~(uintptr_t)3;
+            const uint32_t sh = (uint32_t)(a & 3);
+            const uint32_t *w = (const uint32_t *)aw;
+            const uint64_t vlim = (uint64_t)((uintptr_t)in + in_len - aw);   // valid bytes from w
+            const uint64_t wlim = vlim / 4;                                   // whole dwords from w
+            const uint32_t ndw = (got + 3) / 4;
+            uint32_t *d32 = (uint32_t *)dst;
+            constexpr uint32_t kU = 4;   // strips per lane and step, all loads in flight together
+            for (uint32_t j00 = 4 * tid; j00 < ndw; j00 += 4 * kDSymThreads * kU) {
+                uint32_t v[kU][5];
+#pragma unroll
+                for (uint32_t u = 0; u < kU; u++)
+#pragma unroll
+                    for (uint32_t k = 0; k < 5; k++) {
+                        const uint64_t wi = (uint64_t)j00 + 4 * kDSymThreads * u + k;
+                        if (wi < wlim) v[u][k] = w[wi];
+                        else {   // the buffer's last partial dword, byte by byte
+                            v[u][k] = 0;
+                            for (uint32_t q = 0; q < 4; q++)
+                                if (4 * wi + q < vlim) v[u][k] |= (uint32_t)((const uint8_t *)aw)[4 * wi + q] << (8 * q);
+                        }
+                    }
+#pragma unroll
+                for (uint32_t u = 0; u < kU; u++) {
+                    const uint32_t j0 = j00 + 4 * kDSymThreads * u;
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; k++) {
+                        if (j0 + k >= ndw) break;
+                        const uint32_t c = __builtin_amdgcn_alignbyte(v[u][k + 1], v[u][k], sh);
+                        uint32_t o = 0;
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; q++)
+                            if (4 * (j0 + k) + q < got) o |= (uint32_t)(T[(c >> (8 * q)) & 0xFFu] & 0xFFu) << (8 * q);
+                        d32[j0 + k] = o;   // (bytes past `got` are zero, as the tail below writes them)
+                    }
+                }
+            }
+        } else {
+            uint64_t bit0;
+            const BitBuf src = make_bits(in, in_len, bit0);
+            got = seg_decode<false>(src, bit0 + s.words_bit, s.nbits, s.count, T, C, dst, nullptr, st, cnt, flag, stats);
+        }
     }
     // symbols the words do not cover stay zero (the reference memsets, 1107-1187)
     for (uint32_t x = got + tid; x < s.count; x += kDSymThreads) dst[x] = 0;
