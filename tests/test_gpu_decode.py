@@ -79,6 +79,22 @@ def test_round_trip_random_mosaics(dctx):
         assert dctx.decompress_host(blob, n + 16) == want, f"iteration {it}: n={n} block={block}"
 
 
+def test_byte_code_streams(dctx):
+    """chars sub-streams whose Huffman codes are all 8 bits (random bytes: a complete
+    depth-8 tree) take k_dsyms' byte-substitution path; mixed with blocks whose chars
+    codes vary (text) and with random blocks cut short (the stream's last partial word,
+    words at every byte alignment of the record), against the oracle's restatement of
+    the reference decoder (my_decompress_file_lz77 :2255-2393)"""
+    rnd = inputs.generate("rand", 21, 3 * 65536 + 777)
+    txt = inputs.generate("text", 22, 100000)
+    cases = [(rnd, 65536), (rnd + txt + rnd[:70001], 65536), (rnd[:65536 * 2 + 13], 65536),
+             (txt[:5000] + rnd, 262144), (rnd, 1 << 20)]
+    for i, (data, block) in enumerate(cases):
+        blob = oracle.compress_file(data, block)
+        want = oracle.decompress_file(blob, len(data) + 16)
+        assert dctx.decompress_host(blob, len(data) + 16) == want, f"case {i}: n={len(data)} block={block}"
+
+
 def test_device_records_api(dctx, cuda):
     """GPU encode -> device records -> GPU decode, no host round trip in between"""
     import torch
