@@ -53,7 +53,8 @@ struct Rec78 {
 struct Scratch {
     uint32_t B, nb, cap_log2, Gmax, tiles;
     uint64_t *slot;      // nb << cap_log2
-    uint32_t *d1;        // nb << 16 (depth-1 children, dense)
+    uint32_t *d1;        // nb << 16 (depth-1 children, dense; null when dense1 == 0)
+    uint32_t dense1;     // blocks >= kDense1Min: dense depth-1 table, else depth 1 is hashed too
     uint32_t *idx;       // nb * B
     uint8_t *c;          // nb * B
     uint32_t *bm;        // nb * bmw
@@ -81,6 +82,11 @@ struct Scratch {
 
 __device__ inline uint64_t trie_hash(uint64_t key) { return (key * 0x9E3779B97F4A7C15ull) >> 17; }
 
+// block size from which the depth-1 children get the dense 256 KiB table: a small block has
+// few 2-byte phrases (<= B/2), so they share the hash table (then <= B/2 entries in B + 2
+// slots), and a batch of tiny blocks no longer allocates and zeroes 256 KiB per block
+constexpr uint32_t kDense1Min = 65536;
+
 // ---------------------------------------------------------------------------
 // my_LZ78_compress (1832-1899): phrase = longest dictionary prefix + 1 byte; token
 // (prefix index or 0, byte); the phrase enters the dictionary at the next index.  A
@@ -88,7 +94,9 @@ __device__ inline uint64_t trie_hash(uint64_t key) { return (key * 0x9E3779B97F4
 // The dictionary is a set of strings with ids, so it can be held as three tables
 // with the same contents as one trie: the root's children in LDS (256 ids), the
 // depth-1 children as a dense 256x256 table per block (256 KiB, L2/MALL-resident),
-// deeper children in the open-addressed hash table.  One wave per block, lane 0 walks.
+// deeper children in the open-addressed hash table (blocks < kDense1Min: depth 1 too).
+// One wave per block, lane 0 walks.
+template <bool DENSE1>
 __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, uint64_t n, Scratch S, uint64_t base_blk) {
     __shared__ uint32_t root[256];
     const uint32_t b = blockIdx.x;
@@ -104,7 +112,7 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
     const uint32_t len = (uint32_t)min((uint64_t)S.B, n - off);
     const uint8_t *src = in + off;
     uint64_t *slot = S.slot + ((uint64_t)b << S.cap_log2);
-    uint32_t *d1 = S.d1 + ((uint64_t)b << 16);
+    uint32_t *d1 = DENSE1 ? S.d1 + ((uint64_t)b << 16) : nullptr;
     const uint64_t mask = (1ull << S.cap_log2) - 1;
     uint32_t *idx = S.idx + (uint64_t)b * S.B;
     uint8_t *cc = S.c + (uint64_t)b * S.B;
@@ -121,7 +129,7 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
         // load, one depth-1 load, then the hashed levels
         const uint32_t b0 = src[pos], b1 = pos + 1 < len ? src[pos + 1] : 0u;
         const uint32_t b2 = pos + 2 < len ? src[pos + 2] : 0u, b3 = pos + 3 < len ? src[pos + 3] : 0u;
-        const uint32_t c0 = root[b0], c1 = d1[(b0 << 8) | b1];
+        const uint32_t c0 = root[b0], c1 = DENSE1 ? d1[(b0 << 8) | b1] : 0u;
         if (!c0) {   // new 1-byte phrase
             root[b0] = next++;
             emit(0, b0);
@@ -132,17 +140,26 @@ __global__ __launch_bounds__(64) void k78_parse(const uint8_t *__restrict__ in, 
             emit(c0, 0);
             break;
         }
-        if (!c1) {   // new 2-byte phrase
-            d1[(b0 << 8) | b1] = next++;
-            emit(c0, b1);
+        uint32_t node, ahead, nahead;   // bytes already loaded past the node's phrase
+        if (DENSE1) {
+            if (!c1) {   // new 2-byte phrase
+                d1[(b0 << 8) | b1] = next++;
+                emit(c0, b1);
+                pos += 2;
+                continue;
+            }
+            node = c1;
             pos += 2;
-            continue;
+            ahead = b2 | (b3 << 8);
+            nahead = 2;
+        } else {     // hashed depth 1: the walk below starts at the root child
+            node = c0;
+            pos += 1;
+            ahead = b1 | (b2 << 8) | (b3 << 16);
+            nahead = 3;
         }
-        uint32_t node = c1;
-        pos += 2;
         bool put = false;
         uint64_t h = 0, key = 0;
-        uint32_t ahead = b2 | (b3 << 8), nahead = 2;   // bytes already loaded past the first two
         while (pos < len) {
             const uint32_t byte = nahead ? (ahead & 0xFF) : src[pos];
             ahead >>= 8;
@@ -653,12 +670,13 @@ int setup(Alloc78 &A, Cache78 &C, uint32_t B, uint32_t nb) {
     if (S.Gmax < 1024) S.Gmax = 1024;   // the char tree borrows iw[0..511]; parents need 2*256
     S.tiles = (B + 1 + kTileTok - 1) / kTileTok;
     S.bmw = B / 32 + 2;
+    S.dense1 = B >= kDense1Min ? 1u : 0u;
     const uint64_t nbl = nb;
     uint64_t sz[] = {
         (nbl << S.cap_log2) * 8, nbl * B * 4, nbl * B, nbl * S.bmw * 4, nbl * S.bmw * 4, nbl * B * 2, nbl * B,
         nbl * S.Gmax * 4, nbl * 256 * 4, nbl * S.Gmax * 4, nbl * S.Gmax, nbl * 256 * 4, nbl * 256,
         nbl * 2 * S.Gmax * 4, nbl * 2 * S.Gmax * 4, nbl * S.Gmax * 4, nbl * 576, nbl * S.tiles * 8,
-        nbl * (B + 2) * 4, nbl * (B + 2) * 4, nbl * sizeof(Rec78), nbl * 8, 8, (nbl << 16) * 4};
+        nbl * (B + 2) * 4, nbl * (B + 2) * 4, nbl * sizeof(Rec78), nbl * 8, 8, S.dense1 ? (nbl << 16) * 4 : 0};
     constexpr int K = sizeof(sz) / sizeof(sz[0]);
     uint64_t offs[K], tot = 0;
     for (int i = 0; i < K; i++) {
@@ -697,7 +715,7 @@ int setup(Alloc78 &A, Cache78 &C, uint32_t B, uint32_t nb) {
     S.rec = (Rec78 *)(m + offs[20]);
     S.off = (uint64_t *)(m + offs[21]);
     S.total = (uint64_t *)(m + offs[22]);
-    S.d1 = (uint32_t *)(m + offs[23]);
+    S.d1 = S.dense1 ? (uint32_t *)(m + offs[23]) : nullptr;
     return FCX_OK;
 }
 
@@ -723,7 +741,8 @@ int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_byte
     // table, group tables: large for tiny blocks) within a 64 GiB budget
     uint32_t cl2 = 10;
     while ((1ull << cl2) < (uint64_t)block_bytes + 2) cl2++;
-    const uint64_t per_block = (8ull << cl2) + (1ull << 18) + 64ull * std::max<uint32_t>(1024, block_bytes / 256 + 2) +
+    const uint64_t per_block = (8ull << cl2) + (block_bytes >= kDense1Min ? 1ull << 18 : 0) +
+                               64ull * std::max<uint32_t>(1024, block_bytes / 256 + 2) +
                                24ull * block_bytes + 4096;
     const uint64_t by_budget = std::max<uint64_t>(1, kScratchBudget / per_block);
     const uint32_t batch = (uint32_t)std::max<uint64_t>(
@@ -746,14 +765,15 @@ int fcx_lz78_compress_shard(const uint8_t *d_in, uint64_t n, uint32_t block_byte
         S.nb = (uint32_t)std::min<uint64_t>(batch, nblk - b0);
         const uint32_t nb = S.nb;
         H78(hipMemsetAsync(S.slot, 0, ((uint64_t)nb << S.cap_log2) * 8, st));
-        H78(hipMemsetAsync(S.d1, 0, ((uint64_t)nb << 16) * 4, st));
+        if (S.dense1) H78(hipMemsetAsync(S.d1, 0, ((uint64_t)nb << 16) * 4, st));
         H78(hipMemsetAsync(S.bm, 0, (uint64_t)nb * S.bmw * 4, st));
         H78(hipMemsetAsync(S.gcnt, 0, (uint64_t)nb * S.Gmax * 4, st));
         H78(hipMemsetAsync(S.chist, 0, (uint64_t)nb * 256 * 4, st));
         H78(hipMemsetAsync(S.gstage, 0, (uint64_t)nb * (S.B + 2) * 4, st));
         H78(hipMemsetAsync(S.cstage, 0, (uint64_t)nb * (S.B + 2) * 4, st));
         const dim3 tok_grid(S.tiles, nb);
-        k78_parse<<<nb, 64, 0, st>>>(d_in, n, S, b0);
+        if (S.dense1) k78_parse<true><<<nb, 64, 0, st>>>(d_in, n, S, b0);
+        else k78_parse<false><<<nb, 64, 0, st>>>(d_in, n, S, b0);
         k78_mark<<<tok_grid, 256, 0, st>>>(S);
         k78_rank<<<nb, 1024, 0, st>>>(S);
         k78_group<<<tok_grid, 256, 0, st>>>(S);
