@@ -49,6 +49,7 @@ constexpr uint32_t kDErrRecord = 1, kDErrHeader = 2, kDErrTree = 4, kDErrGolomb 
 constexpr uint32_t kDSymThreads = 1024;
 constexpr uint32_t kDLzThreads = 1024;
 constexpr uint32_t kDLzTile = 8192;              // output bytes resolved per LDS step
+constexpr uint32_t kDLzTPT = 6;                  // tokens read per lane and step (a tile of literals)
 constexpr uint32_t kDTblBits = 10;
 constexpr uint32_t kMaxTokensPerBlock = FCX_MAX_BLOCK_BYTES;
 
@@ -792,7 +793,7 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
                                                      uint32_t *err) {
     __shared__ uint8_t ob[kHist + kDLzTile];              // [history | this step's bytes]
     __shared__ __attribute__((aligned(16))) uint32_t lk[kDLzTile];   // token marks, then links / bytes
-    __shared__ uint2 tr[4 * kDLzThreads];                 // this step's tokens: off | L << 13 | ism << 22 | ok << 23, P | c << 16
+    __shared__ uint2 tr[kDLzTPT * kDLzThreads];                 // this step's tokens: off | L << 13 | ism << 22 | ok << 23, P | c << 16
     __shared__ uint32_t sh[16];
     __shared__ uint32_t s_any[2];
     __shared__ uint32_t s_used;
@@ -806,16 +807,16 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
     uint8_t *o = out + B.out_off;
     const uint32_t n_eff = B.n_eff;
     uint32_t tc = 0, mc = 0, oc = 0;
-    uint32_t window = 4 * kDLzThreads;   // tokens read per step, adapted to the token length seen
+    uint32_t window = kDLzTPT * kDLzThreads;   // tokens read per step, adapted to the token length seen
     bool bad = false;
     while (tc < n_eff) {
         const uint32_t limit = min(n_eff, tc + window);
-        uint32_t len[4], L[4], P[4], c[4];
-        bool ism[4], valid[4];
+        uint32_t len[kDLzTPT], L[kDLzTPT], P[kDLzTPT], c[kDLzTPT];
+        bool ism[kDLzTPT], valid[kDLzTPT];
         uint32_t nm = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-            const uint32_t t = tc + 4 * tid + u;
+        for (uint32_t u = 0; u < kDLzTPT; u++) {
+            const uint32_t t = tc + kDLzTPT * tid + u;
             valid[u] = t < limit;
             ism[u] = valid[u] && !((fl[t >> 3] >> (t & 7)) & 1u);
             c[u] = valid[u] ? ch[t] : 0u;
@@ -827,8 +828,8 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
             // literal tokens only (random data): the bytes are the chars, one per token
             const uint32_t cnt = limit - tc;
 #pragma unroll
-            for (uint32_t u = 0; u < 4; u++)
-                if (valid[u]) o[oc + 4 * tid + u] = (uint8_t)c[u];
+            for (uint32_t u = 0; u < kDLzTPT; u++)
+                if (valid[u]) o[oc + kDLzTPT * tid + u] = (uint8_t)c[u];
             // history = the last 2 KiB of [history | these bytes]
             uint8_t h[kHist / kDLzThreads];
 #pragma unroll
@@ -842,12 +843,12 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
             __syncthreads();
             oc += cnt;
             tc += cnt;
-            window = 4 * kDLzThreads;
+            window = kDLzTPT * kDLzThreads;
             continue;
         }
         uint32_t lsum = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
+        for (uint32_t u = 0; u < kDLzTPT; u++) {
             L[u] = 0; P[u] = 0;
             if (ism[u]) {
                 L[u] = gl[rank];
@@ -867,7 +868,7 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
         // the tokens whose output fits the tile (a prefix): record + mark at their first byte
         uint32_t taken = 0, mtaken = 0, end = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
+        for (uint32_t u = 0; u < kDLzTPT; u++) {
             if (valid[u] && off + len[u] <= kDLzTile) {
                 taken++;
                 // a distance before the block start is malformed (reference: Fatal Error,
@@ -875,9 +876,9 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
                 const bool okp = !ism[u] || (P[u] != 0 && P[u] <= oc + off);
                 bad = bad || !okp;
                 mtaken += ism[u] ? 1u : 0u;
-                tr[4 * tid + u] = make_uint2(off | (L[u] << 13) | ((ism[u] ? 1u : 0u) << 22) | ((okp ? 1u : 0u) << 23),
+                tr[kDLzTPT * tid + u] = make_uint2(off | (L[u] << 13) | ((ism[u] ? 1u : 0u) << 22) | ((okp ? 1u : 0u) << 23),
                                              P[u] | (c[u] << 16));
-                lk[off] = 4 * tid + u + 1;
+                lk[off] = kDLzTPT * tid + u + 1;
                 end = off + len[u];
             }
             off += len[u];
@@ -952,8 +953,8 @@ __global__ __launch_bounds__(kDLzThreads) void k_dlz(uint32_t nblocks, const DBl
         tc += ttot;
         mc += mt2;
         if (ttot == 0) { bad = true; break; }   // cannot happen for l <= 257 (k_dlen)
-        // next window: enough tokens for about two tiles at this step's mean length
-        window = min(4 * kDLzThreads, max(256u, (uint32_t)(2ull * kDLzTile * ttot / max(used, 1u))));
+        // next window: enough tokens for about 1.25 tiles at this step's mean length
+        window = min(kDLzTPT * kDLzThreads, max(256u, (uint32_t)(5ull * kDLzTile * ttot / (4ull * max(used, 1u)))));
     }
     if (bad) atomicOr(err, kDErrDist);
 }
