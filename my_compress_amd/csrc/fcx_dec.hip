@@ -551,8 +551,10 @@ __device__ uint32_t seg_decode(const BitBuf &src, uint64_t sb, uint32_t nbits, u
     return min(tot, count);
 }
 
-// one workgroup per sub-stream: Huffman symbols into the symbol scratch
-__global__ __launch_bounds__(kDSymThreads) void k_dsyms(const uint8_t *in, uint64_t in_len, uint32_t nblocks,
+// one workgroup per sub-stream: Huffman symbols into the symbol scratch.  64 VGPRs (a few
+// spilled) for two workgroups per CU: the serial code walks are latency-bound, and twice
+// the waves took text's symbol streams from 15.1 to 9.9 ms per GiB
+__global__ __launch_bounds__(kDSymThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_dsyms(const uint8_t *in, uint64_t in_len, uint32_t nblocks,
                                                         const DStream *ds, const uint16_t *tbl, const uint16_t *child,
                                                         uint8_t *sym, const uint32_t *err, uint64_t *stats) {
     __shared__ uint16_t T[1u << kDTblBits];
