@@ -577,7 +577,7 @@ __global__ __launch_bounds__(kDSymThreads) __attribute__((amdgpu_waves_per_eu(8)
         __syncthreads();
         // every code 8 bits long (a complete depth-8 tree: the chars of random data): the
         // codes are the stream's bytes (the words start on a byte), so symbol i is T[byte i]
-        // - a byte substitution, 16 bytes per lane and step, no segment agreement
+        // - a byte substitution, no segment agreement
         static_assert(kDSymThreads == (1u << kDTblBits), "one table entry per lane");
         const uint32_t e = T[tid];
         if (__syncthreads_and(!(e & 0x8000u) && ((e >> 8) & 0x1Fu) == 8u)) {
@@ -589,34 +589,34 @@ __global__ __launch_bounds__(kDSymThreads) __attribute__((amdgpu_waves_per_eu(8)
             const uint64_t wlim = vlim / 4;                                   // whole dwords from w
             const uint32_t ndw = (got + 3) / 4;
             uint32_t *d32 = (uint32_t *)dst;
-            constexpr uint32_t kU = 4;   // strips per lane and step, all loads in flight together
-            for (uint32_t j00 = 4 * tid; j00 < ndw; j00 += 4 * kDSymThreads * kU) {
-                uint32_t v[kU][5];
-#pragma unroll
-                for (uint32_t u = 0; u < kU; u++)
-#pragma unroll
-                    for (uint32_t k = 0; k < 5; k++) {
-                        const uint64_t wi = (uint64_t)j00 + 4 * kDSymThreads * u + k;
-                        if (wi < wlim) v[u][k] = w[wi];
-                        else {   // the buffer's last partial dword, byte by byte
-                            v[u][k] = 0;
-                            for (uint32_t q = 0; q < 4; q++)
-                                if (4 * wi + q < vlim) v[u][k] |= (uint32_t)((const uint8_t *)aw)[4 * wi + q] << (8 * q);
-                        }
-                    }
+            // output dword j = lane + 1024 i: consecutive lanes touch consecutive dwords (loads
+            // and stores coalesce); kU dwords per lane and step, all loads in flight together
+            auto ld = [&](uint64_t wi) -> uint32_t {
+                if (wi < wlim) return w[wi];
+                uint32_t x = 0;   // the buffer's last partial dword, byte by byte
+                for (uint32_t q = 0; q < 4; q++)
+                    if (4 * wi + q < vlim) x |= (uint32_t)((const uint8_t *)aw)[4 * wi + q] << (8 * q);
+                return x;
+            };
+            constexpr uint32_t kU = 4;
+            for (uint32_t j00 = tid; j00 < ndw; j00 += kDSymThreads * kU) {
+                uint32_t v0[kU], v1[kU];
 #pragma unroll
                 for (uint32_t u = 0; u < kU; u++) {
-                    const uint32_t j0 = j00 + 4 * kDSymThreads * u;
+                    const uint32_t j = j00 + kDSymThreads * u;
+                    v0[u] = j < ndw ? ld(j) : 0u;
+                    v1[u] = j < ndw ? ld((uint64_t)j + 1) : 0u;
+                }
 #pragma unroll
-                    for (uint32_t k = 0; k < 4; k++) {
-                        if (j0 + k >= ndw) break;
-                        const uint32_t c = __builtin_amdgcn_alignbyte(v[u][k + 1], v[u][k], sh);
-                        uint32_t o = 0;
+                for (uint32_t u = 0; u < kU; u++) {
+                    const uint32_t j = j00 + kDSymThreads * u;
+                    if (j >= ndw) break;
+                    const uint32_t c = __builtin_amdgcn_alignbyte(v1[u], v0[u], sh);
+                    uint32_t o = 0;
 #pragma unroll
-                        for (uint32_t q = 0; q < 4; q++)
-                            if (4 * (j0 + k) + q < got) o |= (uint32_t)(T[(c >> (8 * q)) & 0xFFu] & 0xFFu) << (8 * q);
-                        d32[j0 + k] = o;   // (bytes past `got` are zero, as the tail below writes them)
-                    }
+                    for (uint32_t q = 0; q < 4; q++)
+                        if (4 * j + q < got) o |= (uint32_t)(T[(c >> (8 * q)) & 0xFFu] & 0xFFu) << (8 * q);
+                    d32[j] = o;   // (bytes past `got` are zero, as the tail below writes them)
                 }
             }
         } else {
