@@ -91,8 +91,9 @@ __global__ __launch_bounds__(kEncT) void k_hist(Layout L, const BlockInfo *__res
                                                 const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
                                                 uint32_t *__restrict__ hist) {
     constexpr uint32_t kW = kEncT / 64;
-    __shared__ uint32_t h[kW][256];
-    const uint32_t tid = threadIdx.x, wv = tid >> 6;
+    constexpr uint32_t kCopies = 4;   // sub-histograms per wave (lane & 3): fewer same-address atomics
+    __shared__ uint32_t h[kW][kCopies][256];
+    const uint32_t tid = threadIdx.x, wv = tid >> 6, cp = tid & (kCopies - 1);
     const uint32_t b = blockIdx.x / L.cpb_total;
     uint32_t s, c;
     chunk_of(L, blockIdx.x % L.cpb_total, s, c);
@@ -105,24 +106,26 @@ __global__ __launch_bounds__(kEncT) void k_hist(Layout L, const BlockInfo *__res
     const uint32_t i0 = c0 + kSymL * tid, i1 = min(c1, i0 + kSymL);
     uint32_t sym[kSymW];
     const uint32_t n = chunk_symbols((const uint32_t *)stream_base(L, s, b, s0, s1, s2, s3), i0, i1, sym);
-    for (uint32_t x = tid; x < kW * 256; x += kEncT) (&h[0][0])[x] = 0;
+    for (uint32_t x = tid; x < kW * kCopies * 256; x += kEncT) (&h[0][0][0])[x] = 0;
     __syncthreads();
     uint32_t cur = sym[0] & 0xFF, run = 0;
     for (uint32_t q = 0; q < n; q++) {
         const uint32_t v = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
         if (v != cur) {
-            atomicAdd(&h[wv][cur], run);
+            atomicAdd(&h[wv][cp][cur], run);
             cur = v;
             run = 0;
         }
         run++;
     }
-    if (run) atomicAdd(&h[wv][cur], run);
+    if (run) atomicAdd(&h[wv][cp][cur], run);
     __syncthreads();
     for (uint32_t x = tid; x < 256; x += kEncT) {
         uint32_t t = 0;
 #pragma unroll
-        for (uint32_t w = 0; w < kW; w++) t += h[w][x];
+        for (uint32_t w = 0; w < kW; w++)
+#pragma unroll
+            for (uint32_t c = 0; c < kCopies; c++) t += h[w][c][x];
         hist[(uint64_t)blockIdx.x * 256 + x] = t;
     }
 }
