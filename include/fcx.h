@@ -59,8 +59,10 @@ typedef struct fcx_ctx fcx_ctx;
  * (len <= FCX_MAX_BLOCK_BYTES) and writes the block payload to `out`, which the
  * caller sizes at >= 2*len + 1024 (the reference allots 2 MiB per 1 MiB block,
  * :4088).  Returns payload bytes, or 0 if a pointer is NULL (:2122-2123) or on
- * error (see fcx_last_error).  Runs on the current HIP device through a
- * lazily created per-thread context. */
+ * error (see fcx_last_error).  len == 0 is a valid block, as in the reference: its
+ * 17-byte payload (N = 0, pCnt = 0, HUFF of one zero byte, G = 0) is written without
+ * touching the device.  Runs on the current HIP device through a lazily created
+ * per-thread context. */
 uint32_t fcx_compress_block(const void *in, uint32_t len, uint8_t *out);
 
 /* Same contract as my_decompress_file_lz77 (:2255) but into memory: decodes one

@@ -302,8 +302,6 @@ def decompress_gpu(blob: bytes, cap: int = None, device: int = 0, ctx: "DContext
 def my_compress_file_lz77(block: bytes) -> bytes:
     """one block (<= 1 MiB) -> payload, same bytes as my_compress_file_lz77 (:2115)"""
     n = len(block)
-    if n == 0:
-        return b""
     out = ctypes.create_string_buffer(2 * n + 4096)
     got = lib().fcx_compress_block(block, n, out)
     if got == 0:

@@ -48,39 +48,63 @@ struct fcx_dist {
     int base_rank = 0;               // rank of local index 0
     std::vector<int> devices;        // per local rank
     std::vector<ncclComm_t> comms;   // per local rank
-    std::vector<uint64_t *> d_sizes; // per local rank: nranks u64 (size all-gather)
+    std::vector<uint64_t *> d_sizes; // per local rank: 2 x nranks u64 (size + capacity all-gather)
+    // fcx_dist_compress_host's per-device resources, kept across calls
+    uint32_t block = 0;
+    std::vector<fcx_ctx *> ctx;
+    std::vector<uint8_t *> din, dout;
+    std::vector<hipStream_t> st;
+    std::vector<uint64_t> dincap, dcap;
 };
 
 namespace {
 
-// sizes all-gather + segment placement for local rank li (one host thread per local rank)
+constexpr uint64_t kFailed = ~0ull;   // size-exchange word of a rank whose compress failed
+
+// sizes all-gather + segment placement for local rank li (one host thread per local rank).
+// Every rank always enters both phases, whatever happened before: `status` != FCX_OK (this
+// rank's compress failed) travels as a sentinel size, and each rank also publishes the
+// capacity it receives into, so the exchange hands every rank the same facts and every
+// rank reaches the same verdict (skip the data phase and fail, or run it) -- no rank is
+// left waiting in a send or receive that its peer never posts.
 int concat_local(fcx_dist *d, int li, const uint8_t *d_seg, uint64_t seg_len, uint8_t *d_out, uint64_t cap,
-                 uint64_t *total, int mode, hipStream_t st) {
+                 uint64_t *total, int mode, hipStream_t st, int status = FCX_OK) {
     const int n = d->nranks, rank = d->base_rank + li;
     ncclComm_t comm = d->comms[li];
     DHIP(hipSetDevice(d->devices[li]));
     uint64_t *ds = d->d_sizes[li];
-    DHIP(hipMemcpyAsync(ds + rank, &seg_len, sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    DNCCL(ncclAllGather(ds + rank, ds, 1, ncclUint64, comm, st));
-    std::vector<uint64_t> sizes(n), offs(n, 0);
-    DHIP(hipMemcpyAsync(sizes.data(), ds, n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    const bool receives = mode == FCX_DIST_ALLGATHER || rank == 0;
+    const uint64_t mine[2] = {status ? kFailed : seg_len, receives ? cap : kFailed};
+    DHIP(hipMemcpyAsync(ds + 2 * rank, mine, sizeof(mine), hipMemcpyHostToDevice, st));
+    DNCCL(ncclAllGather(ds + 2 * rank, ds, 2, ncclUint64, comm, st));
+    std::vector<uint64_t> words(2 * (size_t)n), sizes(n), offs(n, 0);
+    DHIP(hipMemcpyAsync(words.data(), ds, words.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     DHIP(hipStreamSynchronize(st));
+    if (status) return status;   // (this rank's own message is already set)
+    for (int r = 0; r < n; r++) {
+        if (words[2 * r] == kFailed)
+            return dfail(FCX_ERR_RCCL, "fcx_dist_concat: rank " + std::to_string(r) + " failed; no segment exchanged");
+        sizes[r] = words[2 * r];
+    }
     for (int r = 1; r < n; r++) offs[r] = offs[r - 1] + sizes[r - 1];
     const uint64_t tot = offs[n - 1] + sizes[n - 1];
     *total = tot;
-    if (sizes[rank] != seg_len) return dfail(FCX_ERR_INTERNAL, "fcx_dist_concat: size exchange mismatch");
-    const bool receives = mode == FCX_DIST_ALLGATHER || rank == 0;
-    if (receives && tot > cap) return dfail(FCX_ERR_CAPACITY, "fcx_dist_concat: output capacity too small");
-    // own segment to its offset (skipped when it already lives there)
-    if (receives && seg_len && d_seg != d_out + offs[rank])
-        DHIP(hipMemcpyAsync(d_out + offs[rank], d_seg, seg_len, hipMemcpyDeviceToDevice, st));
+    for (int r = 0; r < n; r++)   // every receiving rank's capacity, judged identically everywhere
+        if (words[2 * r + 1] != kFailed && tot > words[2 * r + 1])
+            return dfail(FCX_ERR_CAPACITY, "fcx_dist_concat: output capacity of rank " + std::to_string(r) +
+                                               " too small (" + std::to_string(tot) + " B)");
+    // own segment to its offset (skipped when it already lives there); the exchanged size
+    // is what every peer expects, so it is the one sent and received
+    const uint64_t own = sizes[rank];
+    if (receives && own && d_seg != d_out + offs[rank])
+        DHIP(hipMemcpyAsync(d_out + offs[rank], d_seg, own, hipMemcpyDeviceToDevice, st));
     DNCCL(ncclGroupStart());
     if (mode == FCX_DIST_GATHER) {
         if (rank == 0) {
             for (int r = 1; r < n; r++)
                 if (sizes[r]) DNCCL(ncclRecv(d_out + offs[r], sizes[r], ncclUint8, r, comm, st));
-        } else if (seg_len) {
-            DNCCL(ncclSend(d_seg, seg_len, ncclUint8, 0, comm, st));
+        } else if (own) {
+            DNCCL(ncclSend(d_seg, own, ncclUint8, 0, comm, st));
         }
     } else {
         for (int r = 0; r < n; r++)
@@ -88,6 +112,47 @@ int concat_local(fcx_dist *d, int li, const uint8_t *d_seg, uint64_t seg_len, ui
     }
     DNCCL(ncclGroupEnd());
     DHIP(hipStreamSynchronize(st));
+    if (own != seg_len) return dfail(FCX_ERR_INTERNAL, "fcx_dist_concat: size exchange mismatch");
+    return FCX_OK;
+}
+
+void release_local(fcx_dist *d) {
+    for (size_t i = 0; i < d->ctx.size(); i++) {
+        (void)hipSetDevice(d->devices[i]);
+        if (d->st[i]) (void)hipStreamDestroy(d->st[i]);
+        if (d->din[i]) (void)hipFree(d->din[i]);
+        if (d->dout[i]) (void)hipFree(d->dout[i]);
+        fcx_ctx_destroy(d->ctx[i]);
+    }
+    d->ctx.clear(); d->din.clear(); d->dout.clear(); d->st.clear(); d->dincap.clear(); d->dcap.clear();
+    d->block = 0;
+}
+
+// (re)allocates fcx_dist_compress_host's resources when the block size changes or a call
+// needs more than the cached ones hold: `per` input bytes per device, and output for the
+// whole round (`round` input bytes) on device 0, one device's range elsewhere
+int ensure_local(fcx_dist *d, uint32_t block, uint64_t per, uint64_t round) {
+    const size_t nd = d->devices.size();
+    bool ok = d->block == block && d->ctx.size() == nd;
+    for (size_t i = 0; ok && i < nd; i++)
+        ok = d->dincap[i] >= per && d->dcap[i] >= fcx_shard_bound(i == 0 ? round : per, block);
+    if (ok) return FCX_OK;
+    release_local(d);
+    d->ctx.assign(nd, nullptr); d->din.assign(nd, nullptr); d->dout.assign(nd, nullptr);
+    d->st.assign(nd, nullptr); d->dincap.assign(nd, 0); d->dcap.assign(nd, 0);
+    d->block = block;
+    for (size_t i = 0; i < nd; i++) {   // one device at a time
+        int r = FCX_OK;
+        if (hipSetDevice(d->devices[i]) != hipSuccess || hipStreamCreate(&d->st[i]) != hipSuccess)
+            r = dfail(FCX_ERR_HIP, "fcx_dist_compress_host: stream");
+        if (!r) r = fcx_ctx_create(&d->ctx[i], d->devices[i], block, per);
+        d->dincap[i] = per;
+        d->dcap[i] = fcx_shard_bound(i == 0 ? round : per, block);
+        if (!r && (hipMalloc((void **)&d->din[i], per) != hipSuccess ||
+                   hipMalloc((void **)&d->dout[i], d->dcap[i]) != hipSuccess))
+            r = dfail(FCX_ERR_NOMEM, "fcx_dist_compress_host: device buffers");
+        if (r) { release_local(d); return r; }
+    }
     return FCX_OK;
 }
 
@@ -95,7 +160,7 @@ int make_dist(fcx_dist **out, fcx_dist *d) {
     d->d_sizes.resize(d->devices.size(), nullptr);
     for (size_t i = 0; i < d->devices.size(); i++) {
         DHIP(hipSetDevice(d->devices[i]));
-        DHIP(hipMalloc((void **)&d->d_sizes[i], sizeof(uint64_t) * (size_t)d->nranks));
+        DHIP(hipMalloc((void **)&d->d_sizes[i], 2 * sizeof(uint64_t) * (size_t)d->nranks));
     }
     *out = d;
     return FCX_OK;
@@ -159,6 +224,7 @@ int fcx_dist_init_local(fcx_dist **out, int ndev, const int *devices) {
 
 void fcx_dist_destroy(fcx_dist *d) {
     if (!d) return;
+    release_local(d);
     for (size_t i = 0; i < d->comms.size(); i++) {
         (void)hipSetDevice(d->devices[i]);
         (void)hipDeviceSynchronize();
@@ -195,36 +261,18 @@ int fcx_dist_compress_host(fcx_dist *d, const uint8_t *in, uint64_t n, uint32_t 
     const int nd = d->nranks;
     const uint64_t per = ((round_bytes ? round_bytes : (1ull << 30)) + block_bytes - 1) / block_bytes * block_bytes;
     const uint64_t round_max = per * (uint64_t)nd;
-    // per device: context, input and output buffers (device 0's output receives the round)
-    std::vector<fcx_ctx *> ctx(nd, nullptr);
-    std::vector<uint8_t *> din(nd, nullptr), dout(nd, nullptr);
-    std::vector<hipStream_t> st(nd, nullptr);
-    std::vector<uint64_t> dcap(nd, 0);
+    const uint64_t rn0 = n < round_max ? n : round_max;
+    // per device: context, input and output buffers (device 0's output receives the round),
+    // kept in the fcx_dist between calls (the CLI's -g N calls once per round of input)
+    int r0 = ensure_local(d, block_bytes, per < rn0 ? per : rn0, rn0);
+    if (r0) return r0;
+    std::vector<fcx_ctx *> &ctx = d->ctx;
+    std::vector<uint8_t *> &din = d->din, &dout = d->dout;
+    std::vector<hipStream_t> &st = d->st;
+    std::vector<uint64_t> &dcap = d->dcap;
     std::vector<int> rc(nd, FCX_OK);
     std::vector<std::string> err(nd);
     uint64_t done_in = 0, done_out = 0;
-    auto release = [&]() {
-        for (int i = 0; i < nd; i++) {
-            (void)hipSetDevice(d->devices[i]);
-            if (st[i]) (void)hipStreamDestroy(st[i]);
-            if (din[i]) (void)hipFree(din[i]);
-            if (dout[i]) (void)hipFree(dout[i]);
-            fcx_ctx_destroy(ctx[i]);
-        }
-    };
-    {   // allocation, one device at a time
-        const uint64_t rn = n < round_max ? n : round_max;
-        for (int i = 0; i < nd; i++) {
-            int r = FCX_OK;
-            if (hipSetDevice(d->devices[i]) != hipSuccess || hipStreamCreate(&st[i]) != hipSuccess)
-                r = dfail(FCX_ERR_HIP, "fcx_dist_compress_host: stream");
-            if (!r) r = fcx_ctx_create(&ctx[i], d->devices[i], block_bytes, per);
-            dcap[i] = fcx_shard_bound(i == 0 ? rn : per, block_bytes);
-            if (!r && (hipMalloc((void **)&din[i], per) != hipSuccess || hipMalloc((void **)&dout[i], dcap[i]) != hipSuccess))
-                r = dfail(FCX_ERR_NOMEM, "fcx_dist_compress_host: device buffers");
-            if (r) { release(); return r; }
-        }
-    }
     while (done_in < n) {
         const uint64_t rn = n - done_in < round_max ? n - done_in : round_max;
         const uint64_t nb = (rn + block_bytes - 1) / block_bytes;
@@ -240,7 +288,8 @@ int fcx_dist_compress_host(fcx_dist *d, const uint8_t *in, uint64_t n, uint32_t 
             if (!r && hi > lo && hipMemcpyAsync(din[i], in + done_in + lo, hi - lo, hipMemcpyHostToDevice, st[i]) != hipSuccess)
                 r = dfail(FCX_ERR_HIP, "fcx_dist_compress_host: H2D");
             if (!r && hi > lo) r = fcx_compress_shard(ctx[i], din[i], hi - lo, dout[i], dcap[i], &seg, st[i]);
-            if (!r) r = concat_local(d, i, dout[i], seg, dout[0], dcap[0], &tot, FCX_DIST_GATHER, st[i]);
+            // every rank enters the exchange, failed or not (a failure is published there)
+            r = concat_local(d, i, dout[i], seg, dout[0], dcap[0], &tot, FCX_DIST_GATHER, st[i], r);
             if (i == 0) total = tot;
             rc[i] = r;
             if (r) err[i] = fcx_last_error();
@@ -251,20 +300,15 @@ int fcx_dist_compress_host(fcx_dist *d, const uint8_t *in, uint64_t n, uint32_t 
         for (auto &t : th) t.join();
         for (int i = 0; i < nd; i++)
             if (rc[i]) {
-                const int r = dfail(rc[i], "device " + std::to_string(d->devices[i]) + ": " + err[i]);
-                release();
-                return r;
+                return dfail(rc[i], "device " + std::to_string(d->devices[i]) + ": " + err[i]);
             }
-        if (done_out + total > cap) { release(); return dfail(FCX_ERR_CAPACITY, "fcx_dist_compress_host: output capacity too small"); }
+        if (done_out + total > cap) return dfail(FCX_ERR_CAPACITY, "fcx_dist_compress_host: output capacity too small");
         (void)hipSetDevice(d->devices[0]);
-        if (hipMemcpy(out + done_out, dout[0], total, hipMemcpyDeviceToHost) != hipSuccess) {
-            release();
+        if (hipMemcpy(out + done_out, dout[0], total, hipMemcpyDeviceToHost) != hipSuccess)
             return dfail(FCX_ERR_HIP, "fcx_dist_compress_host: D2H");
-        }
         done_out += total;
         done_in += rn;
     }
-    release();
     *out_len = done_out;
     return FCX_OK;
 }

@@ -21,6 +21,29 @@ def pytest_configure(config):
         __graft_entry__.build()
 
 
+# Under `pytest -x` the first failure ends the run, so the hot-path evidence goes first:
+# the reference's golden cases and the BASELINE config digests (C2, C3, C4 rank segments,
+# C5a/b, the 1 GiB headline files), then the rest of the compress parity, and only then
+# the §8(f) components (decoder, stream, dist, LZ78) whose failure must not mask them.
+_FILE_ORDER = ["test_oracle.py", "test_capi.py", "test_gpu_parity.py", "test_gpu_stream.py",
+               "test_gpu_dist.py", "test_gpu_decode.py", "test_cli.py", "test_dist.py",
+               "test_gpu_lz78.py", "test_lz78.py"]
+_PARITY_FIRST = ["test_golden_cases_bit_exact", "test_small_hex_fixtures", "test_block_api_matches_reference",
+                 "test_empty_inputs", "test_cfg2_64MiB_rand_64KiB_digest", "test_full_size_digests",
+                 "test_cfg4_rank_segments"]
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def key(item):
+        fname = os.path.basename(str(item.fspath))
+        frank = _FILE_ORDER.index(fname) if fname in _FILE_ORDER else len(_FILE_ORDER)
+        name = item.originalname or item.name
+        trank = _PARITY_FIRST.index(name) if name in _PARITY_FIRST else len(_PARITY_FIRST)
+        return (frank, trank)
+
+    items.sort(key=key)   # stable: keeps definition order inside each rank
+
+
 @pytest.fixture(scope="session")
 def golden():
     with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:

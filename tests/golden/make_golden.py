@@ -130,6 +130,10 @@ def main():
     cbo2 = (ctypes.c_uint8 * ((11 * len(pv)) // 8 + 1))()
     REF.ref_combine_bits(cb2, len(pv), 11, cbo2)
     kat["combine_bits_11"] = {"in": pv, "bits": 11, "out": list(cbo2)}
+    # my_compress_file_lz77 (2115-2253) on totalBytes = 0: a valid call with a 17-byte payload
+    eb = ctypes.create_string_buffer(4096)
+    en = REF.ref_compress_block(b"", 0, eb)
+    kat["empty_block"] = {"in_bytes": 0, "out_hex": eb.raw[:en].hex()}
     wts = [0, 5, 29, 7, 0, 8, 14, 23, 3, 11, 0]
     w = (ctypes.c_uint32 * 11)(*wts)
     nodes = (ctypes.c_uint32 * (4 * 21))()

@@ -100,3 +100,20 @@ def test_null_arguments_follow_reference_contract():
     # my_compress_file_lz77 returns 0 on NULL pointers (:2122-2123)
     assert mc.lib().fcx_compress_block(None, 10, None) == 0
     assert mc.lib().fcx_decompress_block(None, 0, None, 0) == -1
+
+
+def test_empty_block_follows_reference(golden):
+    """my_compress_file_lz77 (:2115-2253) with totalBytes = 0 is a valid call: the reference
+    writes a 17-byte payload (N = 0, pCnt = 0, HUFF of one zero byte, G = 0).  The drop-in
+    returns the same bytes (no device work is needed for them); the oracle agrees."""
+    import oracle
+
+    want = bytes.fromhex(golden["kat"]["empty_block"]["out_hex"])
+    assert len(want) == 17
+    out = ctypes.create_string_buffer(64)
+    assert mc.lib().fcx_compress_block(b"", 0, out) == 17
+    assert out.raw[:17] == want
+    assert mc.my_compress_file_lz77(b"") == want
+    assert oracle.compress_block(b"") == want
+    # an empty file is the header alone: block_num = 0 (4079-4086, 4128-4129)
+    assert oracle.compress_file(b"", 1 << 20) == b"FCX7" + bytes(6) == mc.compress(b"")

@@ -56,6 +56,11 @@ def test_rank_concat_gather_and_allgather(cuda):
         assert torch.equal(out[:seg.numel()], seg)
         with pytest.raises(mc.FcxError):   # capacity
             d.concat(seg.data_ptr(), seg.numel(), out.data_ptr(), 1000, mc.DIST_GATHER, st)
+        # the capacity verdict is taken after the exchange by every rank alike:
+        # the communicator is not left with a half-posted send and the next concat works
+        out.zero_()
+        assert d.concat(seg.data_ptr(), seg.numel(), out.data_ptr(), out.numel(), mc.DIST_ALLGATHER, st) == seg.numel()
+        assert torch.equal(out[:seg.numel()], seg)
     finally:
         d.close()
 

@@ -93,6 +93,44 @@ def test_block_api_matches_reference(golden):
         assert mc.my_compress_file_lz77(data) == blob[14:14 + plen], case["name"]
 
 
+def test_empty_inputs(golden, cuda, tmp_path):
+    """empty block and empty file through every compress entry point: the block drop-in
+    returns the reference's 17-byte payload (my_compress.cpp:2115-2253, totalBytes = 0);
+    a shard of 0 bytes emits no record; an empty file is the 10-byte header with
+    block_num = 0 (4079-4086, 4128-4129) from the C ABI and from the CLI (one GPU and the
+    -g path), and decompresses to nothing"""
+    import subprocess
+
+    import torch
+
+    want_block = bytes.fromhex(golden["kat"]["empty_block"]["out_hex"])
+    assert mc.my_compress_file_lz77(b"") == want_block
+    header = oracle.compress_file(b"", 1 << 20)
+    assert header == mc.write_header(0, 0)
+    ctx = mc.Context(0, 1 << 20, 1 << 20)
+    try:
+        d_out = torch.empty(4096, dtype=torch.uint8, device=cuda)
+        d_in = torch.empty(16, dtype=torch.uint8, device=cuda)
+        assert ctx.compress_shard(d_in.data_ptr(), 0, d_out.data_ptr(), 4096,
+                                  torch.cuda.current_stream().cuda_stream) == 0
+        assert ctx.compress_host(b"") == b""
+    finally:
+        ctx.close()
+    assert mc.compress(b"") == header
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "my_compress_amd", "bin",
+                       "my_compress")
+    (tmp_path / "empty").write_bytes(b"")
+    for extra in ([], ["-g", "1"]):
+        r = subprocess.run([cli, "-i", "empty", "-o", "e.fcx", "-c", "lz77"] + extra, cwd=tmp_path,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert (tmp_path / "e.fcx").read_bytes() == header, extra
+        r = subprocess.run([cli, "-i", "e.fcx", "-o", "back"], cwd=tmp_path, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0 and "SUCCESS" in r.stdout, r.stdout + r.stderr
+        assert (tmp_path / "back").read_bytes() == b""
+
+
 def test_random_inputs_vs_oracle(gpu_compress):
     rng = random.Random(1234)
     for it in range(40):
