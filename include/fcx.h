@@ -133,7 +133,13 @@ int fcx_ctx_set_profiling(fcx_ctx *ctx, int enable);
  * via the run table / the stitch), 2 run table for whole tiles.  The output is identical in
  * every mode; only the speed differs. */
 int fcx_ctx_set_match_mode(fcx_ctx *ctx, int mode);
-/* After a profiled call: number of stages, and stage i's name and device ms. */
+/* Pipelined launch: fcx_compress_shard splits the shard's blocks into `groups` groups
+ * (0 = automatic, currently one group; at most 8, at least 64 blocks each) and launches
+ * consecutive groups on two internal streams, so one group's kernels overlap the next
+ * group's.  The output is identical for every setting. */
+int fcx_ctx_set_groups(fcx_ctx *ctx, int groups);
+/* After a profiled call: number of stages, and stage i's name and device ms (summed over
+ * the call's block groups). */
 int fcx_ctx_stage_count(fcx_ctx *ctx);
 int fcx_ctx_stage(fcx_ctx *ctx, int i, const char **name, float *ms);
 /* statistics of the last call (device counters copied back on request):

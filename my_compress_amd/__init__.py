@@ -68,6 +68,7 @@ def lib():
                                     ctypes.POINTER(ctypes.c_uint64)]
     L.fcx_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.fcx_ctx_set_match_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.fcx_ctx_set_groups.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.fcx_ctx_stage_count.argtypes = [ctypes.c_void_p]
     L.fcx_ctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                 ctypes.POINTER(ctypes.c_float)]
@@ -211,6 +212,10 @@ class Context:
     def set_match_mode(self, mode: int):
         """testing: 0 auto, 1 bucket search, 2 run table for whole tiles (same output)"""
         _check(lib().fcx_ctx_set_match_mode(self._h, mode), "fcx_ctx_set_match_mode")
+
+    def set_groups(self, groups: int):
+        """pipelined launch: block groups over two streams (0 = automatic); same output"""
+        _check(lib().fcx_ctx_set_groups(self._h, groups), "fcx_ctx_set_groups")
 
     def stage_times(self):
         """[(stage name, device ms)] of the last profiled compress_shard"""

@@ -37,6 +37,7 @@ __host__ __device__ inline uint32_t m_dist(uint32_t m) { return m & 0x7FFu; }
 constexpr uint32_t kTileLazy = 1u;   // tile_flags: spec parse unavailable, stitch walks it
 constexpr uint32_t kTileMFull = 2u;  // tile_flags: m[] holds every match / unknown of the tile (run table ran)
 constexpr uint32_t kTileUniform = 4u;  // tile_flags: the tile's window is one byte value; m is m_uniform, no m[] rows
+constexpr uint32_t kTileSpan2 = 8u;    // tile_flags: m[] rows exact below kRmSpan (run-mode tiles), not just kResolveSpan
 
 // m of block position i when the whole window [i - 2047, i + 258) and the block start
 // side of it hold one byte value: every window position matches up to the cap, and the
@@ -48,6 +49,7 @@ __host__ __device__ inline uint32_t m_uniform(uint32_t i, uint32_t blen) {
     return m_pack(L, i < kWin ? i : kWin);
 }
 constexpr uint32_t kResolveSpan = 256;           // k_resolve's walk limit; m[] rows always kept below it
+constexpr uint32_t kRmSpan = 512;                // run-mode tiles keep m[] rows below this (kTileSpan2)
 constexpr uint32_t kTileMatches = kTile / 4;     // compact match list slots per tile (a match covers >= 4)
 constexpr uint32_t kConvAll = 0xFFFFu;           // tile conv record: k_emit takes every m from m[]
 
@@ -120,6 +122,18 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// maximum over the 64 lanes (uniform), by DPP lane moves as wave_incl_scan (no LDS
+// permutes); every lane of the wave must be active
+__device__ inline uint32_t wave_max_dpp(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));   // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // inclusive running maximum across the 64 lanes
 __device__ inline uint32_t wave_incl_max(uint32_t v) {
     const uint32_t lane = lane_id();
@@ -170,7 +184,12 @@ __device__ inline uint32_t lds_match_len(const uint32_t *w, uint32_t a, uint32_t
 constexpr uint32_t kRunBudget = 512;       // runs per window before the position stays "unknown"
 constexpr uint32_t kRunTile = 1024;        // image runs up to which a tile skips the bucket search
 
-__device__ inline uint32_t run_rank(const uint32_t *bm, const uint16_t *prc, uint32_t y) {
+// LDS address space: pointers of this type address LDS with 32-bit offsets (no generic-pointer
+// conversion per access in out-of-line device functions)
+#define FCX_LDS __attribute__((address_space(3)))
+
+template <typename P32, typename P16>
+__device__ inline uint32_t run_rank(P32 bm, P16 prc, uint32_t y) {
     // number of run boundaries at positions <= y
     const uint32_t sh = y & 31;
     const uint32_t msk = sh == 31 ? 0xFFFFFFFFu : ((2u << sh) - 1u);

@@ -339,7 +339,9 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t nblocks, const Bl
                                                       uint64_t cap, uint32_t *__restrict__ err) {
     __shared__ uint64_t wsum[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    uint64_t carry = 0;
+    // offsets continue after the records of the shard's earlier block groups (fcx_compress_shard's
+    // pipelined launch: their scans ran before this one); 0 for the first group
+    uint64_t carry = *total;
     for (uint32_t b0 = 0; b0 < nblocks; b0 += 1024) {
         const uint32_t b = b0 + tid;
         const uint64_t v = b < nblocks ? binfo[b].rec_bytes : 0;
@@ -564,7 +566,7 @@ __global__ __launch_bounds__(64) void k_headers(const BlockInfo *__restrict__ bi
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
                     uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_off,
                     uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
-                    hipEvent_t *ev) {
+                    hipEvent_t *ev, hipEvent_t wait_scan, hipEvent_t rec_scan) {
     const uint32_t nchunks = L.nblocks * L.cpb_total;
     hipLaunchKernelGGL(k_hist, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, hist);
     if (ev) (void)hipEventRecord(ev[0], st);
@@ -573,7 +575,9 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
     if (ev) (void)hipEventRecord(ev[1], st);
     hipLaunchKernelGGL(k_block_layout, dim3((L.nblocks + 63) / 64), dim3(64), 0, st, L.nblocks, binfo);
     if (ev) (void)hipEventRecord(ev[2], st);
+    if (wait_scan) (void)hipStreamWaitEvent(st, wait_scan, 0);   // the previous group's record offsets
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, L.nblocks, binfo, blk_off, total, cap, err);
+    if (rec_scan) (void)hipEventRecord(rec_scan, st);
     if (ev) (void)hipEventRecord(ev[3], st);
     hipLaunchKernelGGL(k_zero_edges, dim3((nchunks + 255) / 256), dim3(256), 0, st, L, binfo, chunk_off, blk_off, out,
                        err);

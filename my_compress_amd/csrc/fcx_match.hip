@@ -89,9 +89,12 @@ __device__ inline uint32_t lanes_below(uint64_t m) {
 // only in tiles that have unknown positions.  mx = m of image position 0, ilen =
 // block length - image base, w0 = image base in the block.  mbx (whole-tile mode,
 // no bucket search ran): mbits of image position 0, written here per 64 positions.
+template <bool kDev>
 __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, uint16_t *step, uint32_t *s_red,
                                          uint32_t *s_unknown, uint32_t *mx, uint64_t *mbx, uint32_t q0, uint32_t npos,
-                                         uint32_t nload, uint32_t ilen, uint32_t w0, uint32_t dbg) {
+                                         uint32_t nload, uint32_t ilen, uint32_t w0, uint32_t dbg_in, uint16_t *dist,
+                                         uint32_t rt_cap) {
+    const uint32_t dbg = kDev ? dbg_in : 0u;   // development bits exist only in k_match<true>
     const uint32_t tid = threadIdx.x;
     uint32_t *rbm = region + kTile / 2;                       // boundary bitmap, kRunBmWords
     uint16_t *prc = (uint16_t *)(rbm + kRunBmWords);          // prefix counts per bitmap word
@@ -113,7 +116,7 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
     for (uint32_t w = 0; w < (tid >> 6); w++) pre += s_red[w];
     const uint32_t nruns = s_red[0] + s_red[1] + s_red[2] + s_red[3];
     if (tid < kRunBmWords) prc[tid] = (uint16_t)pre;
-    if (nruns <= kRunTableCap && tid < kRunBmWords)
+    if (nruns <= rt_cap && tid < kRunBmWords)
         for (uint32_t v = rbm[tid], o = pre; v; v &= v - 1, o++) {
             const uint32_t y = 32 * tid + __builtin_ctz(v);
             rt[o] = y | (y < nload ? lds_ld1(sdw, y) << 16 : 0x1000000u);
@@ -140,8 +143,8 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
         const uint32_t ko = run_rank(rbm, prc, xv) - 1;
         const uint32_t kfirst = __shfl(ko, 0, 64), klast = __shfl(ko, 63, 64);
         uint32_t res = 0;
-        bool lost = need && nruns > kRunTableCap;
-        const bool table = nruns <= kRunTableCap;
+        bool lost = need && nruns > rt_cap;
+        const bool table = nruns <= rt_cap;
         // this lane's own run: r bytes left from xv, own run start / byte
         const uint32_t own = table ? rt[ko] : 0u;
         const uint32_t r = (table ? rt[ko + 1] & 0xFFFFu : xv) - xv;
@@ -247,11 +250,225 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
         } else if (need && !lost) {
             mx[x] = res;
         }
-        if (need && !lost) step[x - q0] = (uint16_t)(res ? m_len(res) + 1 : 1);
+        if (need && !lost) {
+            step[x - q0] = (uint16_t)(res ? m_len(res) + 1 : 1);
+            if (dist) dist[x - q0] = (uint16_t)m_dist(res);
+        }
         left = left || lost;
     }
     if (left) *s_unknown = 1;
     __syncthreads();
+}
+
+// ---- 3c. run-mode tiles (whole-tile run table: zeros-free low-entropy data, e.g. runs).
+// Only the resolve span [t0, t0 + kResolveSpan) is evaluated at every position (dense_phase:
+// k_resolve reads those m rows); past it, m is evaluated at the chain positions only (about
+// one position in 66 on runs data), by one wave per position over the run table.
+constexpr uint32_t kRunTableOff = kTile / 2 + kRunBmWords + kRunBmWords / 2 + 2 + kRunListWords;   // rt in region
+constexpr uint32_t kRmDist = kRegionWords - kTile / 2;           // u16 x kTile: distance of every evaluated position
+constexpr uint32_t kRmOnA = kRmDist - kTile / 16;                // kTile bits: the sub-tile walks' A1 chains
+constexpr uint32_t kRmOnB = kRmOnA + kTile / 32;                 // kTile bits: the fix-up walks' positions
+constexpr uint32_t kRmRunCap = kRmOnA - kRunTableOff - 4;        // run table entries kept clear of both
+constexpr uint32_t kRmSub = kTile / kWaves;                      // 512 positions per wave's sub-tile walk
+static_assert(kRmRunCap >= kRunTile + 8, "run-mode table");
+
+// exact m of image position x (block position w0 + x) over the run table, by the whole wave:
+// one window run per lane (64 per pass), each lane's best candidate in its run packed as
+// L << 13 | (8191 - j), the wave maximum = the longest, then leftmost match (the rules of
+// run_match, fcx_device.h).  ilen = block length - w0.  kUnknown: more than kRunBudget runs.
+__device__ inline uint32_t run_match_wave(const FCX_LDS uint32_t *bm, const FCX_LDS uint16_t *prc,
+                                          const FCX_LDS uint32_t *rt, uint32_t x, uint32_t ilen, uint32_t w0) {
+    const uint32_t lane = lane_id();
+    if (w0 + x == 0 || ilen - x < 4) return 0u;
+    const uint32_t cap = min(kMaxL, ilen - x) - 1;
+    const uint32_t xlo = max(w0 + x, kWin) - kWin - w0;
+    const uint32_t ko = run_rank(bm, prc, x) - 1, klo = run_rank(bm, prc, xlo) - 1;
+    if (ko - klo > kRunBudget) return kUnknown;
+    const uint32_t own = rt[ko], vb0 = rt[ko + 1];
+    const uint32_t c = own >> 16, r = (vb0 & 0xFFFFu) - x;
+    const bool big = r > cap;
+    uint32_t best = 0;
+    for (uint32_t k0 = klo; k0 < ko; k0 += 64) {
+        const uint32_t kc = k0 + lane;
+        if (kc >= ko) continue;
+        const uint32_t v = rt[kc];
+        if ((v >> 16) != c) continue;
+        const uint32_t nv = rt[kc + 1];
+        const uint32_t sp = max(v & 0xFFFFu, xlo), ep = nv & 0xFFFFu;
+        if (ep <= xlo) continue;
+        const uint32_t A = ep - sp;
+        uint32_t Lc, j = sp;
+        if (big) Lc = min(A, cap);
+        else if (A < r) Lc = A;
+        else {
+            // ext at run granularity (equal (byte, length) runs extend it, the first length
+            // mismatch adds the shorter length); the query side meets the image end only past the cap
+            uint32_t ext = 0;
+            if (r < cap) {
+                const uint32_t lim = cap - r;
+                uint32_t ka = kc + 1, kb = ko + 1, va = nv, vb = vb0;
+                while ((va >> 16) == (vb >> 16)) {
+                    const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
+                    const uint32_t la = (na & 0xFFFFu) - (va & 0xFFFFu), lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
+                    if (la != lb) { ext += min(la, lb); break; }
+                    ext += la;
+                    if (ext >= lim) break;
+                    ka++; kb++; va = na; vb = nb;
+                }
+                ext = min(ext, lim);
+            }
+            Lc = min(r + ext, cap);
+            if (ext) j = ep - r;
+        }
+        best = max(best, (Lc << 13) | (8191u - j));
+    }
+    const uint32_t sp = max(own & 0xFFFFu, xlo);   // candidates inside the own run give r
+    if (sp < x) best = max(best, ((big ? cap : r) << 13) | (8191u - sp));
+    best = wave_max_dpp(best);
+    const uint32_t L = best >> 13;
+    return L >= kMinL ? m_pack(L, x - (8191u - (best & 0x1FFFu))) : 0u;
+}
+
+// The speculative chain of a run-mode tile from t0, evaluating m where the walks need it
+// (positions below kRmSpan were evaluated by dense_phase).  All eight waves work in parallel:
+//   A1  wave w walks its 512-position sub-tile from the sub-tile's first position (chain marked
+//       in onA; exit X1_w);
+//   A2  fix-up rounds: wave w walks from the exit of sub-tile w - 1 until it meets its own A1
+//       chain (greedy chains resynchronise within a token or two) -- from there on the A1 chain
+//       is the true one and the exit stays X1_w; a walk that never meets changes the exit, and
+//       the next round re-walks the following sub-tiles (rounds until no exit changes);
+//   C   every wave turns its sub-tile's chain (walked positions before the meeting point, the A1
+//       chain from it) into chain words, counts, prefix counts (block scan) and its part of the
+//       compact match list.
+// Past kRmSpan the mbits words are exact on chain positions and "unknown" elsewhere (no m rows
+// there: the stitch evaluates such positions itself if its walk ever reaches one).  Sets
+// *s_unknown when a window holds too many runs (the caller then publishes a lazy tile).
+// step (L + 1) of tile position x, evaluated over the run table when dense_phase / an earlier
+// walk did not (then stored with its distance); wave-uniform; 0 = unknown
+__device__ inline uint32_t rm_stepat(FCX_LDS uint32_t *region, uint32_t x, uint32_t q0, uint32_t ilen, uint32_t w0) {
+    FCX_LDS uint16_t *step = (FCX_LDS uint16_t *)region;
+    uint32_t sv = step[x];
+    if (sv == 0) {
+        const FCX_LDS uint32_t *rbm = region + kTile / 2;
+        const uint32_t mm = run_match_wave(rbm, (const FCX_LDS uint16_t *)(rbm + kRunBmWords), region + kRunTableOff,
+                                           q0 + x, ilen, w0);
+        if (mm == kUnknown) return 0u;
+        sv = m_len(mm) + 1;
+        if (lane_id() == 0) {
+            step[x] = (uint16_t)sv;
+            ((FCX_LDS uint16_t *)(region + kRmDist))[x] = (uint16_t)m_dist(mm);
+        }
+    }
+    return sv;
+}
+
+__device__ __noinline__ void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32_t *s_ex, FCX_LDS uint32_t *s_unknown,
+                                        uint32_t q0, uint32_t nt, uint32_t ilen, uint32_t w0, uint32_t t0, uint64_t *mbw,
+                                        uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t *mt, uint32_t dbg) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    FCX_LDS uint16_t *step = (FCX_LDS uint16_t *)region;
+    FCX_LDS uint16_t *dist = (FCX_LDS uint16_t *)(region + kRmDist);
+    FCX_LDS uint32_t *onA = region + kRmOnA, *onB = region + kRmOnB;
+    for (uint32_t w = tid; w < 2 * (kTile / 32); w += kMT) onA[w] = 0;   // onA and onB (adjacent)
+    __syncthreads();
+    const uint32_t a = kRmSub * wv, bnd = min(a + kRmSub, nt);
+    bool lost = false;
+    uint32_t X1 = a;
+    {   // A1
+        uint32_t x = a;
+        while (x < bnd) {
+            const uint32_t sv = rm_stepat(region, x, q0, ilen, w0);
+            if (sv == 0) { lost = true; break; }
+            if (lane == 0) onA[x >> 5] |= 1u << (x & 31);   // (the sub-tile's words are this wave's alone)
+            x += sv;
+        }
+        X1 = x;
+        if (lane == 0) s_ex[wv] = x;
+        if (lost && lane == 0) *s_unknown = 1;
+    }
+    __syncthreads();
+    if (*s_unknown || (dbg & (1u << 18))) return;   // (timing: A1 only)
+    uint32_t curE = a, meet = a;   // this sub-tile's entry and where its chain joins the A1 chain
+    for (uint32_t round = 0; round < kWaves; round++) {   // A2
+        const uint32_t E = wv == 0 ? 0u : s_ex[wv - 1];
+        __syncthreads();
+        bool changed = false;
+        if (a < nt && E != curE) {
+            curE = E;
+            if (lane < kRmSub / 32) onB[a / 32 + lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t x = E;
+            while (x < bnd && !((onA[x >> 5] >> (x & 31)) & 1u)) {
+                const uint32_t sv = rm_stepat(region, x, q0, ilen, w0);
+                if (sv == 0) { lost = true; break; }
+                if (lane == 0) onB[x >> 5] |= 1u << (x & 31);
+                x += sv;
+            }
+            meet = x < bnd ? x : bnd;
+            const uint32_t ex = x < bnd ? X1 : x;
+            changed = ex != s_ex[wv];
+            if (lane == 0) {
+                s_ex[wv] = ex;
+                if (lost) *s_unknown = 1;
+            }
+        }
+        if (__syncthreads_or(changed ? 1 : 0) == 0 || *s_unknown) break;
+    }
+    if (*s_unknown || (dbg & (1u << 19))) return;   // (timing: A1 + A2)
+    // C: lanes 0..7 of wave w take the sub-tile's eight chain words
+    const uint32_t gw = a / 64 + lane;                 // tile word of this lane
+    const bool own = lane < kRmSub / 64 && 64 * gw < nt;
+    uint64_t word = 0, mword = 0;
+    uint32_t cnt[3] = {0, 0, 0};
+    if (own) {
+        const uint32_t lo = 64 * gw;
+        const uint64_t A = (uint64_t)onA[2 * gw] | ((uint64_t)onA[2 * gw + 1] << 32);
+        const uint64_t B = (uint64_t)onB[2 * gw] | ((uint64_t)onB[2 * gw + 1] << 32);
+        const uint64_t keep = meet <= lo ? ~0ull : meet >= lo + 64 ? 0ull : ~0ull << (meet - lo);
+        word = curE == a ? A : (B | (A & keep));
+        for (uint64_t bb = word; bb; bb &= bb - 1) {
+            const uint32_t x = lo + (uint32_t)__builtin_ctzll(bb);
+            const uint32_t sv = step[x];
+            cnt[0]++;
+            if (sv > 1) { mword |= 1ull << (x - lo); cnt[1]++; cnt[2] += ((sv - 1) >> 2) + 3; }
+        }
+    }
+    uint32_t inc[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) inc[q] = wave_incl_scan(cnt[q]);
+    if (lane == 63)
+        for (int q = 0; q < 3; q++) s_ex[kWaves + q * kWaves + wv] = inc[q];   // (s_ex holds >= 4 kWaves words)
+    __syncthreads();
+    uint32_t pre[3], tot[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        uint32_t p = 0, t = 0;
+        for (uint32_t w = 0; w < kWaves; w++) {
+            const uint32_t v = s_ex[kWaves + q * kWaves + w];
+            if (w < wv) p += v;
+            t += v;
+        }
+        pre[q] = p + inc[q] - cnt[q];
+        tot[q] = t;
+    }
+    if (own) {
+        cw[gw] = word;
+        pfx[gw] = (uint64_t)pre[0] | ((uint64_t)pre[1] << 13) | ((uint64_t)pre[2] << 24);
+        if (gw >= kRmSpan / 64) mbw[gw] = ~word | mword;
+        uint32_t o = pre[1];
+        for (uint64_t bb = mword; bb; bb &= bb - 1) {
+            const uint32_t x = 64 * gw + (uint32_t)__builtin_ctzll(bb);
+            mt[o++] = m_pack((uint32_t)step[x] - 1u, dist[x]);
+        }
+    }
+    const uint32_t lastw = (nt - 1) / kRmSub;   // the wave whose sub-tile holds the tile end
+    if (tid == 0) {
+        ti[0] = kTileSpan2;
+        ti[1] = t0 + s_ex[lastw];
+        ti[2] = tot[0];
+        ti[3] = tot[1];
+        ti[4] = tot[2];
+    }
 }
 
 // one candidate xe (image position, already known to lie in the window left of x) of
@@ -298,11 +515,13 @@ __device__ inline void scan_candidate(const uint32_t *sdw, uint32_t xe, uint32_t
 // compare, leftmost maximum, extension budget); every other position is a literal.
 // Writes step (LDS), m and the tile's mbits words.  Kept out of line: its registers do
 // not weigh on the bucket search.
+template <bool kDev>
 __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region, uint32_t kw0, uint32_t kw1,
                                            uint32_t kw2, uint32_t kw3, uint32_t *s_red,
                                            uint32_t *s_np, uint32_t *s_unknown, uint32_t *s_match, uint32_t *mrow,
                                            uint64_t *mbw, uint32_t q0, uint32_t npos, uint32_t ins_end, uint32_t w0,
-                                           uint32_t blen, uint32_t ntile, uint32_t dbg) {
+                                           uint32_t blen, uint32_t ntile, uint32_t dbg_in) {
+    const uint32_t dbg = kDev ? dbg_in : 0u;
     const uint32_t tid = threadIdx.x;
     const uint32_t kw[4] = {kw0, kw1, kw2, kw3};
     auto hash_of = [&](uint32_t r) -> uint32_t {
@@ -402,6 +621,75 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
     }
 }
 
+// ---- sparse tiles with a few matches (random data) ----
+// Every position is a literal except the handful of match positions the sparse search found,
+// so the greedy chain from t0 follows from the ordered match list: a match is taken when the
+// chain reaches it (no earlier taken match covers it), everything else is a literal token.
+// Wave 0 publishes what the Jacobi parse publishes (chain words, prefix counts, compact match
+// list, tile totals).  mbl: the search's per-64-position match words (tile-relative), step:
+// L + 1 per position, res: m per position, list: 64 words of scratch.  Returns false (nothing
+// written) above 64 match positions; every wave returns the same verdict.
+__device__ inline bool sparse_parse(const uint64_t *mbl, const uint16_t *step, const uint32_t *res, uint32_t *list,
+                                    uint32_t nt, uint32_t t0, uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t *mt) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nwords = (nt + 63) / 64;
+    const uint64_t wm = lane < nwords ? mbl[lane] : 0ull;
+    const uint32_t cntw = (uint32_t)__popcll(wm);
+    const uint32_t inc = wave_incl_scan(cntw);
+    const uint32_t nm = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    if (nm > 64) return false;
+    if (threadIdx.x >= 64) return true;
+    uint32_t k = inc - cntw;
+    for (uint64_t bits = wm; bits; bits &= bits - 1, k++) list[k] = 64 * lane + (uint32_t)__builtin_ctzll(bits);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t pos = lane < nm ? list[lane] : 0u;
+    const uint32_t Lv = lane < nm ? (uint32_t)step[pos] - 1u : 0u;
+    // the chain takes a match when it reaches it (uniform walk over the ordered list)
+    uint64_t tk = 0;
+    uint32_t cur = 0;
+    for (uint32_t i = 0; i < nm; i++) {
+        const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)i);
+        if (p >= cur) {
+            tk |= 1ull << i;
+            cur = p + (uint32_t)__builtin_amdgcn_readlane((int)Lv, (int)i) + 1;
+        }
+    }
+    // lane w: chain word w (literal tokens minus the taken matches' covered positions) and the
+    // counts of the chain positions before it
+    const uint32_t lo = 64 * lane;
+    uint64_t cov = 0;
+    uint32_t cov_before = 0, cov_tile = 0, mat_before = 0, gb_before = 0, gb_all = 0;
+    for (uint64_t bits = tk; bits; bits &= bits - 1) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(bits);
+        const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)i);
+        const uint32_t Lm = (uint32_t)__builtin_amdgcn_readlane((int)Lv, (int)i);
+        const uint32_t c0 = p + 1, c1 = p + Lm + 1;   // covered positions [c0, c1)
+        const uint32_t a = max(c0, lo), z = min(c1, lo + 64);
+        if (a < z) cov |= (z - a == 64 ? ~0ull : ((1ull << (z - a)) - 1ull)) << (a - lo);
+        cov_before += c1 <= lo ? c1 - c0 : (c0 < lo ? lo - c0 : 0u);
+        cov_tile += min(c1, nt) - c0;
+        const uint32_t g = (Lm >> 2) + 3;
+        if (p < lo) { mat_before++; gb_before += g; }
+        gb_all += g;
+    }
+    const uint32_t ntk = (uint32_t)__popcll(tk);
+    if (lane < nwords) {
+        const uint32_t nb = min(64u, nt - lo);
+        const uint64_t valid = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+        cw[lane] = valid & ~cov;
+        pfx[lane] = (uint64_t)(lo - cov_before) | ((uint64_t)mat_before << 13) | ((uint64_t)gb_before << 24);
+    }
+    if (lane < nm && ((tk >> lane) & 1ull)) mt[__popcll(tk & ((1ull << lane) - 1ull))] = res[pos];
+    if (lane == 0) {
+        ti[0] = 0u;
+        ti[1] = t0 + max(cur, nt);
+        ti[2] = nt - cov_tile;
+        ti[3] = ntk;
+        ti[4] = gb_all;
+    }
+    return true;
+}
+
 // ---- uniform tiles (one byte value over the whole image: zeros) ----
 // m is m_uniform everywhere: no search, no run table, no m[] rows.  The speculative chain
 // from t0 follows directly; this publishes what the parse below publishes for other tiles
@@ -467,10 +755,15 @@ __device__ inline void uniform_tile_out(uint32_t *sc /* >= kMT + 1 words */, uin
     }
 }
 
+// kDev = false is the product kernel: every development / test-mode bit is compiled out.
+// k_match<true> carries them (phase exits for tools/matchphase.py through fcx_debug_match, and
+// the forced tile modes of fcx_ctx_set_match_mode, which the parity tests use).
+template <bool kDev>
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
-                                              uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg) {
+                                              uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg_in) {
+    const uint32_t dbg = kDev ? dbg_in : 0u;
     __shared__ __attribute__((aligned(16))) uint32_t sdw[kTileBytes / 4 + 4];   // byte image of the window
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
     // search, [step (u16 x 4096) | parse scratch] after it
@@ -487,7 +780,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __shared__ uint32_t s_events;   // repeat filter: window keys whose hash was seen before
     __shared__ uint32_t s_np;       // sparse search: positions whose hash repeats
     __shared__ uint32_t s_chg[2];
-    __shared__ uint32_t s_red[3 * kWaves];   // cross-wave scan partials
+    __shared__ uint32_t s_red[4 * kWaves];   // cross-wave scan partials (rmode_walk: exits + 3 scans)
 
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
@@ -599,6 +892,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         return key_mix(__builtin_amdgcn_alignbyte(kw[(r >> 2) + 1], kw[r >> 2], r & 3) & 0xFFFFFFu);
     };
 
+    bool sparse = false;   // the sparse search ran (few repeated keys: random data)
     if (rmode) {
         if (nruns_img == 1 && !(dbg & 12u)) {   // one byte value over the whole image (zeros)
             uniform_tile_out(region, s_red, mbits + (uint64_t)b * L.wpb,
@@ -615,7 +909,6 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // repeat.  Random data has a few hundred repeats per tile (almost all hash
     // collisions), so the search below visits only the positions whose hash repeats
     // (sparse search); above kSparseEvents repeats the tile takes the bucket search. ----
-    bool sparse = false;
     if (s_sample <= kSampleEvents && !(dbg & 128u)) {
     uint32_t *seen = region, *dupm = region + kFilterWords / 2;   // (zeroed with the staging)
     {
@@ -649,7 +942,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }   // repeat filter
 
     if (sparse) {
-        sparse_search(sdw, region, kw[0], kw[1], kw[2], kw[3], s_red, &s_np, &s_unknown, &s_match, m + bstart + w0,
+        sparse_search<kDev>(sdw, region, kw[0], kw[1], kw[2], kw[3], s_red, &s_np, &s_unknown, &s_match, m + bstart + w0,
                       mbits + (uint64_t)b * L.wpb + (t0 >> 6), q0, npos, ins_end, w0, blen, t1 - t0, dbg);
         __syncthreads();
         if (dbg & 32u) return;
@@ -851,14 +1144,32 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
     // ---- 3b. dense windows: exact matches of the unknown positions over the run table ----
     const bool dense = s_unknown != 0;   // matches may come from the run table: no fast path below
-    if (dense)
-        dense_phase(sdw, region, step, s_red, &s_unknown, m + bstart + w0,
-                    rmode ? mbits + (uint64_t)b * L.wpb + (w0 >> 6) : nullptr, q0, npos, nload, blen - w0, w0, dbg);
+    if (dense)   // (run mode: the resolve span only; rmode_walk evaluates the chain past it)
+        dense_phase<kDev>(sdw, region, step, s_red, &s_unknown, m + bstart + w0,
+                    rmode ? mbits + (uint64_t)b * L.wpb + (w0 >> 6) : nullptr, q0,
+                    rmode ? min(npos, q0 + kRmSpan) : npos, nload, blen - w0, w0, dbg,
+                    rmode ? (uint16_t *)(region + kRmDist) : nullptr, rmode ? kRmRunCap : kRunTableCap);
 
     if (dbg & 64u) return;   // timing: + queries (no parse)
     uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
     uint32_t *ti = tinfo + 8ull * blockIdx.x;
     const uint32_t nwords = (t1 - t0 + 63) / 64;
+    if (rmode) {
+        uint64_t *mbw = mbits + (uint64_t)b * L.wpb + (t0 >> 6);
+        if (s_unknown == 0)
+            rmode_walk((FCX_LDS uint32_t *)region, (FCX_LDS uint32_t *)s_red, (FCX_LDS uint32_t *)&s_unknown, q0,
+                       t1 - t0, blen - w0, w0, t0, mbw, cw,
+                       chain_pfx + (uint64_t)blockIdx.x * (kTile / 64), ti, mtok + (uint64_t)blockIdx.x * kTileMatches, dbg);
+        __syncthreads();
+        if (s_unknown != 0) {   // lazy tile: m rows in the span only, "unknown" past it
+            for (uint32_t w = tid; w < nwords; w += kMT) {
+                cw[w] = 0;
+                if (w >= kRmSpan / 64) mbw[w] = ~0ull;
+            }
+            if (tid == 0) { ti[0] = kTileLazy | kTileSpan2; ti[1] = 0; ti[2] = ti[3] = ti[4] = 0; }
+        }
+        return;
+    }
     if (s_unknown != 0) {
         for (uint32_t w = tid; w < nwords; w += kMT) cw[w] = 0;
         if (tid == 0) { ti[0] = kTileLazy | kTileMFull; ti[1] = 0; ti[2] = ti[3] = ti[4] = 0; }
@@ -876,6 +1187,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if (tid == 0) { ti[0] = 0; ti[1] = t1; ti[2] = t1 - t0; ti[3] = 0; ti[4] = 0; }
         return;
     }
+
+    if (sparse && !dense && !(dbg & 65536u) &&
+        sparse_parse((const uint64_t *)(region + kSpMb), step, region + kResLds, region + kSpP, t1 - t0, t0, cw,
+                     chain_pfx + (uint64_t)blockIdx.x * (kTile / 64), ti, mtok + (uint64_t)blockIdx.x * kTileMatches))
+        return;
 
     // ---- 4. tile-local greedy parse ----
     uint32_t *Gs = region + kTile / 2;                 // kMT + 1 entries
@@ -1002,13 +1318,17 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                   uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override) {
-    // dbg bits exist only for fcx_debug_match (development; launches this kernel alone on
-    // scratch the caller discards): bit0 skip searches, bit1 skip long extension, bit2 never /
-    // bit3 always take the whole-tile run mode, bits 4-6 phase exits.  The product path
-    // (fcx_compress_shard) always passes 0; nothing is read from the environment.
+    // dbg bits (k_match<true> only): fcx_debug_match's phase exits and experiment bits
+    // (development; the kernel alone on scratch the caller discards) and the forced tile modes
+    // of fcx_ctx_set_match_mode (bit2 never / bit3 always the whole-tile run mode, bit7 no
+    // repeat filter; output unchanged).  The default path launches k_match<false>, compiled
+    // without any of them; nothing is read from the environment.
     const uint32_t dbg = dbg_override != ~0u ? dbg_override : 0u;
     const uint32_t grid = L.nblocks * L.tpb;
-    hipLaunchKernelGGL(k_match, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg);
+    if (dbg == 0)
+        hipLaunchKernelGGL(k_match<false>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u);
+    else
+        hipLaunchKernelGGL(k_match<true>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg);
 }
 
 }  // namespace fcx

@@ -433,6 +433,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
         const bool lazy = (sti[j][0] & kTileLazy) != 0;
         const bool mfull = (sti[j][0] & kTileMFull) != 0;   // else m[] rows stop at kResolveSpan
         const bool uni = (sti[j][0] & kTileUniform) != 0;  // m = m_uniform, no rows
+        const uint32_t span = (sti[j][0] & kTileSpan2) ? kRmSpan : kResolveSpan;   // m rows exact below it
         uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
         const uint64_t *pfx = chain_pfx + (uint64_t)tix * (kTile / 64);
         const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
 #pragma unroll
                 for (uint32_t u = 0; u < 4; u++)
                     if (x + u < nt)
-                        mL[x + u] = ((mbw >> u) & 1u) ? (mfull || x + u < kResolveSpan ? (x + 4 <= nt ? vv[u] : mt[x + u])
+                        mL[x + u] = ((mbw >> u) & 1u) ? (mfull || x + u < span ? (x + 4 <= nt ? vv[u] : mt[x + u])
                                                                                       : kUnknown)
                                                       : 0u;
             }
@@ -511,7 +512,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
             mbL[lane] = lane < nw ? mb[lane] : 0ull;   // one mbits word per lane (64 words per tile)
             __syncthreads();
             for (uint32_t x = lane; x < nt; x += 64)   // m only where the position's mbits bit is set
-                mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? (mfull || x < kResolveSpan ? mt[x] : kUnknown) : 0u;
+                mL[x] = ((mbL[x >> 6] >> (x & 63)) & 1ull) ? (mfull || x < span ? mt[x] : kUnknown) : 0u;
             for (uint32_t w = lane; w < kTile / 64; w += 64) bmL[w] = w < nw ? cw[w] : 0ull;
         }
         __syncthreads();

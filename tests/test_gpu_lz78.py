@@ -103,6 +103,10 @@ def test_decode_quirks_and_malformed():
         mc.my_decompress_file_lz78(p[:len(p) // 2])    # truncated
     with pytest.raises(mc.FcxError):
         mc.decompress_lz78(mc.compress(b"abc"))         # an FCX7 stream
+    # bytes after the block_num counted records are ignored, as main() does (4162-4201; the u16
+    # count wraps past 65535 blocks and the reference then decodes the counted ones)
+    blob = mc.compress_lz78(inputs.mosaic(6, 9000), 4096)
+    assert mc.decompress_lz78(blob + b"\x07" * 37) == mc.decompress_lz78(blob)
 
 
 @pytest.mark.parametrize("block", [1, 7, 1000, 4096])

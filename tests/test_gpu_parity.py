@@ -144,6 +144,31 @@ def test_random_inputs_vs_oracle(gpu_compress):
         assert got == want, f"iteration {it}: n={n} block={block}"
 
 
+@pytest.mark.parametrize("groups", [2, 3, 8])
+def test_pipelined_groups_same_output(cuda, groups):
+    """fcx_ctx_set_groups: the shard's blocks in groups on two streams (record offsets
+    continue from group to group); the bytes must equal the oracle's"""
+    import torch
+
+    data = inputs.mosaic(4321, 3 * 1000 * 1000 + 777)
+    for block in (4096, 65536):
+        ctx = mc.Context(0, block, len(data))
+        try:
+            ctx.set_groups(groups)
+            d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
+            cap = mc.shard_bound(len(data), block)
+            d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+            n = ctx.compress_shard(d_in.data_ptr(), len(data), d_out.data_ptr(), cap,
+                                   torch.cuda.current_stream().cuda_stream)
+            got = mc.write_header(len(data), (len(data) + block - 1) // block) + d_out[:n].cpu().numpy().tobytes()
+            assert got == oracle.compress_file(data, block), (groups, block)
+            with pytest.raises(mc.FcxError):   # capacity: a later group's scan sees the overflow
+                ctx.compress_shard(d_in.data_ptr(), len(data), d_out.data_ptr(), n // 2,
+                                   torch.cuda.current_stream().cuda_stream)
+        finally:
+            ctx.close()
+
+
 def test_dense_and_periodic_edges(gpu_compress):
     # long matches capped at 257, matches crossing tile borders, cap shrinking at block end
     cases = [

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--block", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check", default=None)
+    ap.add_argument("--groups", default="0", help="comma list of fcx_ctx_set_groups values to time")
     a = ap.parse_args()
     n = a.mib << 20
     t = time.time()
@@ -42,23 +43,28 @@ def main():
     ctx = mc.Context(0, a.block, n)
     st = torch.cuda.current_stream().cuda_stream
     got = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)  # warm
-    ctx.set_profiling(True)
-    for r in range(a.reps):
+    for G in [int(x) for x in a.groups.split(",")]:
+        ctx.set_groups(G)
+        ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)  # warm
         torch.cuda.synchronize()
         t = time.time()
-        got = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)
+        for r in range(a.reps):   # back to back, unprofiled
+            ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st, sync=False)
         torch.cuda.synchronize()
-        dt = time.time() - t
-        print(f"rep {r}: {dt * 1e3:.2f} ms  {n / dt / 1e9:.2f} GB/s  out={got} ratio={got / n:.4f}", flush=True)
-    for name, ms in ctx.stage_times():
-        print(f"   {name:14s} {ms:9.3f} ms")
+        dt = (time.time() - t) / a.reps
+        got = ctx.read_out_len()
+        print(f"groups {G}: {dt * 1e3:.3f} ms  {n / dt / 1e9:.2f} GB/s  out={got} ratio={got / n:.4f}", flush=True)
+        ctx.set_profiling(True)
+        ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)
+        print("   " + "  ".join(f"{name} {ms:.3f}" for name, ms in ctx.stage_times()))
+        ctx.set_profiling(False)
+        if a.check:
+            cfg = inputs.SURVEY_DIGESTS[a.check]
+            h = hashlib.sha256(mc.write_header(n, (n + a.block - 1) // a.block))
+            h.update(memoryview(d_out[:got].cpu().numpy()))
+            print("   digest", "OK" if h.hexdigest() == cfg["out"] and got + 10 == cfg["bytes"] else "MISMATCH",
+                  got + 10, cfg["bytes"], flush=True)
     print(ctx.stats())
-    if a.check:
-        cfg = inputs.SURVEY_DIGESTS[a.check]
-        h = hashlib.sha256(mc.write_header(n, (n + a.block - 1) // a.block))
-        h.update(memoryview(d_out[:got].cpu().numpy()))
-        print("digest", "OK" if h.hexdigest() == cfg["out"] and got + 10 == cfg["bytes"] else "MISMATCH",
-              got + 10, cfg["bytes"])
     ctx.close()
 
 

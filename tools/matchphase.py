@@ -20,7 +20,7 @@ L = mc.lib()
 L.fcx_debug_match.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
 s = torch.cuda.current_stream()
 res = {}
-for name, bits in [("stage+count", 16), ("+filter", 4096), ("+sort", 32), ("+runtable", 8192 | 64), ("+eval-noloop", 16384 | 64), ("+eval-nofold", 32768 | 64), ("+queries", 64), ("+walks", 512), ("+jacobi", 256), ("+counts", 1024), ("+list", 2048), ("whole", 0), ("no-search", 1)]:
+for name, bits in [("stage+count", 16), ("+filter", 4096), ("+sort", 32), ("+runtable", 8192 | 64), ("+eval-noloop", 16384 | 64), ("+eval-nofold", 32768 | 64), ("+queries", 64), ("+rmA1", 1 << 18), ("+rmA2", 1 << 19), ("+walks", 512), ("+jacobi", 256), ("+counts", 1024), ("+list", 2048), ("whole", 0), ("no-search", 1)]:
     ts = []
     for r in range(a.reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
