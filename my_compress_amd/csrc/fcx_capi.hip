@@ -19,11 +19,12 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev);
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev);
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
-                    uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_bits,
-                    uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
-                    hipEvent_t *ev, hipEvent_t wait_scan, hipEvent_t rec_scan);
+                    const uint16_t *thist, const uint32_t *bhist, const uint32_t *tile_off, uint32_t *ctab,
+                    uint8_t *ltab, uint8_t *hhdr, uint64_t *cstat, uint64_t *blk_off, uint64_t *total, uint8_t *out,
+                    uint64_t cap, uint32_t *err, hipStream_t st, hipEvent_t *ev, hipEvent_t wait_scan,
+                    hipEvent_t rec_scan);
 }  // namespace fcx
 
 using namespace fcx;
@@ -97,8 +98,10 @@ struct fcx_ctx {
     uint64_t *fp = nullptr;            // per tile: fast-path record (k_resolve)
     BlockInfo *binfo = nullptr;
     uint8_t *s[kStreams] = {nullptr, nullptr, nullptr, nullptr};
-    uint32_t *hist = nullptr;          // per chunk: 256-bin histogram
-    uint32_t *ctab = nullptr, *chunk_bits = nullptr;   // code table; per chunk: starting bit offset
+    uint16_t *thist = nullptr;         // per tile: chars counts (k_emit)
+    uint32_t *bhist = nullptr;         // per block: 256 bins of each stream (k_emit; flags, distances, golomb)
+    uint64_t *cstat = nullptr;         // per chunk: k_encode's look-back status word
+    uint32_t *ctab = nullptr;          // code table
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
     uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits
@@ -123,15 +126,15 @@ struct fcx_ctx {
 namespace {
 void free_scratch(fcx_ctx *c) {
     void *ptrs[] = {c->m,    c->mbits, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->mtok, c->tconv, c->fp, c->binfo,
-                    c->s[0], c->s[1],  c->s[2],      c->s[3],       c->hist,     c->ctab,     c->chunk_bits,
-                    c->ltab, c->hhdr,  c->blk_off};
+                    c->s[0], c->s[1],  c->s[2],      c->s[3],       c->thist,    c->bhist,    c->cstat,
+                    c->ctab, c->ltab,  c->hhdr,      c->blk_off};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     c->m = nullptr; c->mbits = c->chain = c->chain_pfx = c->fp = nullptr; c->tinfo = c->tile_off = nullptr;
     c->mtok = c->tconv = nullptr;
     c->binfo = nullptr;
     for (auto &p : c->s) p = nullptr;
-    c->hist = c->ctab = c->chunk_bits = nullptr;
+    c->thist = nullptr; c->bhist = nullptr; c->cstat = nullptr; c->ctab = nullptr;
     c->ltab = c->hhdr = nullptr;
     c->blk_off = nullptr;
     c->cap_n = 0;
@@ -163,11 +166,12 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     if ((r = dalloc(&c->binfo, sizeof(BlockInfo) * nb, "binfo"))) return r;
     for (uint32_t s = 0; s < kStreams; s++)
         if ((r = dalloc(&c->s[s], (uint64_t)L.sstride[s] * nb + 64, "stream"))) return r;
-    if ((r = dalloc(&c->hist, 4ull * 256 * L.cpb_total * nb, "hist"))) return r;
+    if ((r = dalloc(&c->thist, 2ull * 256 * nt, "thist"))) return r;
+    if ((r = dalloc(&c->bhist, 4ull * 256 * kStreams * nb, "bhist"))) return r;
+    if ((r = dalloc(&c->cstat, 16ull * L.cpb_total * nb, "cstat"))) return r;
     if ((r = dalloc(&c->ctab, 4ull * 256 * kStreams * nb, "ctab"))) return r;
     if ((r = dalloc(&c->ltab, 256ull * kStreams * nb, "ltab"))) return r;
     if ((r = dalloc(&c->hhdr, (uint64_t)kHuffHdrStride * kStreams * nb, "hhdr"))) return r;
-    if ((r = dalloc(&c->chunk_bits, 4ull * L.cpb_total * nb, "chunk_bits"))) return r;
     if ((r = dalloc(&c->blk_off, 8 * nb, "blk_off"))) return r;
     c->cap_n = (uint64_t)L.nblocks * c->B;
     c->cap_blocks = L.nblocks;
@@ -356,12 +360,12 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         if (ev) HIP_TRY(hipEventRecord(ev[2], sg));
         launch_parse(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
                      c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 8 * t0,
-                     c->tile_off + 3 * t0, c->tconv + t0, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3], sg,
-                     ev ? ev + 3 : nullptr);
-        launch_entropy(Lg, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3], c->hist + b0 * L.cpb_total * 256,
-                       c->ctab + b0 * kStreams * 256, c->ltab + b0 * kStreams * 256,
-                       c->hhdr + b0 * kStreams * kHuffHdrStride, c->chunk_bits + b0 * L.cpb_total, c->blk_off + b0,
-                       total, d_out, cap, err, sg, ev ? ev + 5 : nullptr,
+                     c->tile_off + 3 * t0, c->tconv + t0, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3],
+                     c->thist + t0 * 256, c->bhist + b0 * kStreams * 256, sg, ev ? ev + 3 : nullptr);
+        launch_entropy(Lg, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3], c->thist + t0 * 256,
+                       c->bhist + b0 * kStreams * 256, c->tile_off + 3 * t0, c->ctab + b0 * kStreams * 256,
+                       c->ltab + b0 * kStreams * 256, c->hhdr + b0 * kStreams * kHuffHdrStride,
+                       c->cstat + 2 * b0 * L.cpb_total, c->blk_off + b0, total, d_out, cap, err, sg, ev ? ev + 5 : nullptr,
                        G > 1 && g > 0 ? c->gsync[3 + g - 1] : nullptr, G > 1 ? c->gsync[3 + g] : nullptr);
     }
     if (G > 1) {

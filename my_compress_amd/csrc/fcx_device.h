@@ -83,6 +83,9 @@ struct Layout {
 
 // ---- wave64 helpers --------------------------------------------------------
 __device__ inline uint32_t lane_id() { return __lane_id(); }
+// a value every lane of the wave holds alike, moved to a scalar register: loops and branches on
+// it become scalar (no exec-mask bookkeeping) -- only for values that are wave-uniform
+__device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 __device__ inline uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll

@@ -13,19 +13,20 @@
 // per (block, stream), then serialises the tree (1013-1066) and the code table:
 // code = root->leaf path, left = 0, root decision in bit 0 (LSB-first, 869-924).
 //
-//   k_hist         256-bin histogram of every 8192-symbol chunk (per-wave LDS
-//                  bins, runs of equal bytes counted in registers first)
-//   k_tree         sums a stream's chunk histograms, builds the tree, header
-//                  bytes, code table, W, and every chunk's starting bit offset
-//                  (chunk histogram . code lengths) - no second pass over the data
+//   (histograms)   built by k_emit while each tile's stream bits are in LDS (fcx_parse.hip):
+//                  a u16 row of chars counts per tile, block bins for the other streams
+//   k_tree         sums a stream's counts (plus the bytes that straddle two tiles' bits and
+//                  the stream's zero tail, read back here), builds the tree, header bytes,
+//                  code table and W, and clears the stream's chunk status words
 //   k_block_layout record layout and size per block
 //   k_scan_blocks  record offsets across the shard (+ capacity check)
-//   k_zero_edges   zero the words the encoder ORs into (the two edge words of every
-//                  chunk; every other output byte is stored whole by k_encode or k_headers)
-//   k_encode       each lane packs its 64 codes into whole words (LDS atomics only
-//                  for the two words it shares with neighbours); the chunk's words
-//                  are stored at the record's (unaligned) byte offset: interior
-//                  words plain, chunk-edge words atomicOr
+//   k_encode       a chunk of 8192 symbols per workgroup: its bit count, then its starting bit
+//                  by decoupled look-back over the stream's earlier chunks (8-byte status
+//                  words: aggregate or inclusive prefix, and the chunk's last 32 code bits);
+//                  each lane packs its 64 codes into whole words in LDS; the words are stored
+//                  plainly at the record's (unaligned) byte offset, the first one merged with
+//                  the previous chunk's last bits (the word the two chunks share is this
+//                  chunk's to write; a stream's last chunk also writes its partial last word)
 //   k_headers      lengths, counts and tree headers of every record
 #include "fcx_device.h"
 
@@ -86,58 +87,17 @@ __device__ inline const uint8_t *stream_base(const Layout &L, uint32_t s, uint32
     return (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
 }
 
-__global__ __launch_bounds__(kEncT) void k_hist(Layout L, const BlockInfo *__restrict__ binfo,
-                                                const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
-                                                const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
-                                                uint32_t *__restrict__ hist) {
-    constexpr uint32_t kW = kEncT / 64;
-    constexpr uint32_t kCopies = 4;   // sub-histograms per wave (lane & 3): fewer same-address atomics
-    __shared__ uint32_t h[kW][kCopies][256];
-    const uint32_t tid = threadIdx.x, wv = tid >> 6, cp = tid & (kCopies - 1);
-    const uint32_t b = blockIdx.x / L.cpb_total;
-    uint32_t s, c;
-    chunk_of(L, blockIdx.x % L.cpb_total, s, c);
-    const BlockInfo &bi = binfo[b];
-    if (!stream_active(bi, s)) return;
-    const uint32_t len = bi.slen[s], c0 = c * kChunk;
-    if (c0 >= len) return;
-    const uint32_t c1 = min(len, c0 + kChunk);
-    // each lane counts a strip of kSymL consecutive symbols, runs of one byte value first
-    const uint32_t i0 = c0 + kSymL * tid, i1 = min(c1, i0 + kSymL);
-    uint32_t sym[kSymW];
-    const uint32_t n = chunk_symbols((const uint32_t *)stream_base(L, s, b, s0, s1, s2, s3), i0, i1, sym);
-    for (uint32_t x = tid; x < kW * kCopies * 256; x += kEncT) (&h[0][0][0])[x] = 0;
-    __syncthreads();
-    uint32_t cur = sym[0] & 0xFF, run = 0;
-    for (uint32_t q = 0; q < n; q++) {
-        const uint32_t v = (sym[q >> 2] >> (8 * (q & 3))) & 0xFF;
-        if (v != cur) {
-            atomicAdd(&h[wv][cp][cur], run);
-            cur = v;
-            run = 0;
-        }
-        run++;
-    }
-    if (run) atomicAdd(&h[wv][cp][cur], run);
-    __syncthreads();
-    for (uint32_t x = tid; x < 256; x += kEncT) {
-        uint32_t t = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kW; w++)
-#pragma unroll
-            for (uint32_t c = 0; c < kCopies; c++) t += h[w][c][x];
-        hist[(uint64_t)blockIdx.x * 256 + x] = t;
-    }
-}
-
 // ---------------------------------------------------------------------------
 constexpr uint32_t kTreeT = 128;   // k_tree workgroup: two waves (more trees per CU: the merge is serial)
 constexpr uint32_t kTreeW = kTreeT / 64;
 
-__global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__restrict__ hist,
+__global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__restrict__ thist,
+                                                 const uint32_t *__restrict__ bhist,
+                                                 const uint32_t *__restrict__ tile_off, const uint8_t *__restrict__ s0,
+                                                 const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
                                                  BlockInfo *__restrict__ binfo, uint32_t *__restrict__ ctab,
                                                  uint8_t *__restrict__ ltab, uint8_t *__restrict__ hhdr,
-                                                 uint32_t *__restrict__ chunk_off, uint32_t *__restrict__ err) {
+                                                 uint64_t *__restrict__ cstat, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint32_t w[256];
     __shared__ uint32_t sw[257], ss[257], ln[256];   // (the merge reads the leaf queue two deep)
     __shared__ uint32_t iw[256], il[256], ir[256], par[512];
@@ -153,28 +113,53 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__res
     const uint32_t hb = (b * kStreams + s) * 256;
     uint32_t r0 = 0;
     for (uint32_t q = 0; q < s; q++) r0 += L.cpb[q];
-    const uint32_t nch = (bi.slen[s] + kChunk - 1) / kChunk;
-    const uint32_t *hc = hist + ((uint64_t)b * L.cpb_total + r0) * 256;   // this stream's chunk histograms
-    {   // symbol weights: wave wv sums the chunks c = wv mod kTreeW (lane: symbols lane + 64 q)
+    for (uint32_t c = tid; c < 2 * L.cpb[s]; c += kTreeT) cstat[2 * ((uint64_t)b * L.cpb_total + r0) + c] = 0;   // k_encode's look-back
+    const uint32_t ntl = (bi.len + kTile - 1) / kTile;
+    if (s == 1) {   // chars: wave wv sums the tile rows t = wv mod kTreeW (lane: symbols 4 lane .. 4 lane + 3)
+        const uint2 *rows = (const uint2 *)(thist + (uint64_t)b * L.tpb * 256);
         uint32_t acc[4] = {0, 0, 0, 0};
 #pragma unroll 8
-        for (uint32_t c = wv; c < nch; c += kTreeW)
+        for (uint32_t t = wv; t < ntl; t += kTreeW) {
+            const uint2 v = rows[(uint64_t)t * 64 + lane];
+            acc[0] += v.x & 0xFFFFu; acc[1] += v.x >> 16; acc[2] += v.y & 0xFFFFu; acc[3] += v.y >> 16;
+        }
 #pragma unroll
-            for (uint32_t q = 0; q < 4; q++) acc[q] += hc[c * 256 + lane + 64 * q];
+        for (uint32_t q = 0; q < 4; q++) part[wv][4 * lane + q] = acc[q];
+        __syncthreads();
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) part[wv][lane + 64 * q] = acc[q];
+        for (uint32_t u = 0; u < 256 / kTreeT; u++) {
+            const uint32_t sym = tid + kTreeT * u;
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < kTreeW; q++) t += part[q][sym];
+            w[sym] = t;
+        }
+    } else {
+        // the block bins (bytes wholly inside one tile's bits), then the bytes that straddle a tile
+        // boundary (each counted once: at the first boundary inside it) and the stream's zero tail
+        const uint32_t *bh = bhist + ((uint64_t)b * kStreams + s) * 256;
+#pragma unroll
+        for (uint32_t u = 0; u < 256 / kTreeT; u++) w[tid + kTreeT * u] = bh[tid + kTreeT * u];
+        __syncthreads();
+        const uint32_t comp = s == 0 ? 0u : s == 2 ? 1u : 2u;
+        const uint32_t mul = s == 2 ? kPBits : 1u;
+        const uint32_t total = s == 0 ? bi.ntok : s == 2 ? kPBits * bi.nmatch : bi.gbits;
+        const uint8_t *sb = (s == 0 ? s0 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
+        const uint32_t *to = tile_off + 3ull * b * L.tpb;
+        for (uint32_t k = 1 + tid; k <= ntl; k += kTreeT) {
+            const uint32_t B = k < ntl ? mul * to[3 * k + comp] : total;
+            const uint32_t P = k > 1 ? mul * to[3 * (k - 1) + comp] : 0u;
+            if ((B & 7u) && !((P >> 3) == (B >> 3) && (P & 7u))) atomicAdd(&w[sb[B >> 3]], 1u);
+        }
+        if (tid == 0) {
+            if (s == 2 && (total & 7u) == 0) atomicAdd(&w[0], 1u);   // the (11 pCnt)/8 + 1-th byte (2192)
+            if (s == 3) atomicAdd(&w[0], 4 * ((total + 31) / 32) - (total + 7) / 8);   // zero bytes up to the word end
+        }
+        __syncthreads();
     }
-    __syncthreads();
     uint32_t nz = 0;
 #pragma unroll
-    for (uint32_t u = 0; u < 256 / kTreeT; u++) {
-        const uint32_t sym = tid + kTreeT * u;
-        uint32_t t = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kTreeW; q++) t += part[q][sym];
-        w[sym] = t;
-        nz += t != 0 ? 1u : 0u;
-    }
+    for (uint32_t u = 0; u < 256 / kTreeT; u++) nz += w[tid + kTreeT * u] != 0 ? 1u : 0u;
     const uint32_t real = (uint32_t)__syncthreads_count(nz >= 1) + (uint32_t)__syncthreads_count(nz >= 2);
     // stable sort of the leaves by (weight, symbol): rank = number of smaller keys
 #pragma unroll
@@ -222,6 +207,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__res
     }
     __syncthreads();
     const uint32_t root = 256 + nint - 1;
+    uint32_t bits = 0;   // this thread's symbols' share of the stream's code bits
 #pragma unroll
     for (uint32_t u = 0; u < 256 / kTreeT; u++) {   // code of a symbol: root -> leaf path, root decision in bit 0
         const uint32_t sym = tid + kTreeT * u;
@@ -239,34 +225,13 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint32_t *__res
         ctab[hb + sym] = code;
         ltab[hb + sym] = (uint8_t)len;
         ln[sym] = len;
+        bits += w[sym] * len;
     }
+    const uint32_t wsum = wave_sum_u32(bits);
+    if (lane == 0) s_red[wv] = wsum;
     __syncthreads();
-    // starting bit of every chunk: chunk histogram . code lengths (thread c: chunk c, its
-    // 256 counts in 64 independent 16-B loads), exclusive scan in chunk order
     uint64_t carry = 0;
-    for (uint32_t c0 = 0; c0 < nch; c0 += kTreeT) {
-        const uint32_t c = c0 + tid;
-        uint32_t bitsc = 0;
-        if (c < nch) {
-            const uint4 *h4 = (const uint4 *)(hc + (uint64_t)c * 256);
-#pragma unroll 16
-            for (uint32_t q = 0; q < 64; q++) {
-                const uint4 v = h4[q];
-                bitsc += v.x * ln[4 * q] + v.y * ln[4 * q + 1] + v.z * ln[4 * q + 2] + v.w * ln[4 * q + 3];
-            }
-        }
-        const uint32_t inc = wave_incl_scan(bitsc);
-        if (lane == 63) s_red[wv] = inc;
-        __syncthreads();
-        uint32_t pre = 0, all = 0;
-        for (uint32_t q = 0; q < kTreeW; q++) {
-            if (q < wv) pre += s_red[q];
-            all += s_red[q];
-        }
-        if (c < nch) chunk_off[(uint64_t)b * L.cpb_total + r0 + c] = (uint32_t)(carry + pre + inc - bitsc);
-        carry += all;
-        __syncthreads();
-    }
+    for (uint32_t q = 0; q < kTreeW; q++) carry += s_red[q];
     // header: [u8 ts][ceil(2ts/8) B internal-child bitmap][ts x (u8 l, u8 r)]
     const uint32_t ts = nint, nbm = (2 * ts + 7) / 8;
     uint8_t *hdr = hhdr + (uint64_t)(b * kStreams + s) * kHuffHdrStride;
@@ -367,47 +332,44 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t nblocks, const Bl
     }
 }
 
-__global__ __launch_bounds__(256) void k_zero_edges(Layout L, const BlockInfo *__restrict__ binfo,
-                                                    const uint32_t *__restrict__ chunk_off,
-                                                    const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
-                                                    const uint32_t *__restrict__ err) {
-    if (*err & kErrCapacity) return;
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= (uint64_t)L.nblocks * L.cpb_total) return;
-    const uint32_t b = (uint32_t)(q / L.cpb_total), r = (uint32_t)(q % L.cpb_total);
-    uint32_t s, c;
-    chunk_of(L, r, s, c);
-    const BlockInfo &bi = binfo[b];
-    const uint32_t len = bi.slen[s], c0 = c * kChunk;
-    if (!stream_active(bi, s) || c0 >= len) return;
-    const uint64_t base = 8 * (blk_off[b] + bi.words_rel[s]);
-    const uint64_t g0 = base + chunk_off[q];
-    uint32_t *o32 = (uint32_t *)out;
-    if (c0 + kChunk < len) {   // the chunk ends where the next one starts
-        const uint64_t g1 = base + chunk_off[q + 1];
-        o32[g0 >> 5] = 0;
-        if (g1 > g0) o32[(g1 - 1) >> 5] = 0;
-    } else {                   // last chunk: every word through the end of the stream's words
-        const uint64_t g1 = base + 32ull * bi.nwords[s];
-        for (uint64_t w = g0 >> 5; w <= (g1 > g0 ? (g1 - 1) >> 5 : g0 >> 5); w++) o32[w] = 0;
-    }
-}
-
 // staging words: the whole chunk at <= 8 bits per symbol (one pass; random data's chars
 // are exactly 8); longer codes (<= 32 bits) go through several windows of this size
 constexpr uint32_t kEncWords = kChunk / 4 + 2;
 
-__global__ __launch_bounds__(kEncT) void k_encode(Layout L, const BlockInfo *__restrict__ binfo,
+// k_encode's decoupled look-back: two words per chunk, cleared by k_tree.  [0] status: flag
+// (bit 62: aggregate = this chunk's bit count, bit 63: inclusive prefix = the stream's bits
+// through this chunk) | count; [1] the chunk's last 32 code bits | bit 63 once published (the
+// next chunk merges them into the word the two share)
+constexpr uint64_t kStAgg = 1ull << 62, kStInc = 2ull << 62, kStTail = 1ull << 63;
+__device__ inline uint64_t st_word(uint64_t flag, uint32_t v) { return flag | (v & 0x3FFFFFFFu); }
+
+// the chunk's last 32 code bits (staged bits [e - 32, e), e >= 32) for the next chunk
+__device__ inline void publish_tail(uint64_t *st, const uint32_t *ws, uint32_t e) {
+    const uint32_t lo = ws[(e - 32) >> 5], hi = ws[(e - 1) >> 5];
+    const uint32_t tail = (uint32_t)((((uint64_t)hi << 32) | lo) >> ((e - 32) & 31));
+    __hip_atomic_store(st + 1, kStTail | tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the first output word: the previous chunk's last sh0 bits below this chunk's first bits
+// (waits for the previous chunk's tail; it publishes right after staging its words)
+__device__ inline void merge_head(uint64_t *st, uint32_t *o32, uint32_t w0v, uint32_t sh0) {
+    uint64_t t;
+    do t = __hip_atomic_load(st - 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (!(t & kStTail));
+    o32[0] = w0v | ((uint32_t)t >> (32 - sh0));
+}
+
+__global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void k_encode(Layout L, const BlockInfo *__restrict__ binfo,
                                                  const uint8_t *__restrict__ s0, const uint8_t *__restrict__ s1,
                                                  const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
                                                  const uint32_t *__restrict__ ctab, const uint8_t *__restrict__ ltab,
-                                                 const uint32_t *__restrict__ chunk_off,
+                                                 uint64_t *__restrict__ cstat,
                                                  const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
                                                  const uint32_t *__restrict__ err) {
     constexpr uint32_t kW = kEncT / 64;
     __shared__ uint32_t ct[256], lt[256];
     __shared__ uint32_t ws[kEncWords];
     __shared__ uint32_t red[kW];
+    __shared__ uint32_t s_pre;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / L.cpb_total, r = blockIdx.x % L.cpb_total;
     uint32_t s, c;
@@ -418,6 +380,7 @@ __global__ __launch_bounds__(kEncT) void k_encode(Layout L, const BlockInfo *__r
     const uint32_t len = bi.slen[s], c0 = c * kChunk;
     if (errv || !stream_active(bi, s) || c0 >= len) return;
     const uint32_t c1 = min(len, c0 + kChunk);
+    const bool lastc = c1 == len;   // the stream's last chunk
     const uint32_t hb = (b * kStreams + s) * 256;
     uint32_t ctv[256 / kEncT], ltv[256 / kEncT];
 #pragma unroll
@@ -427,7 +390,7 @@ __global__ __launch_bounds__(kEncT) void k_encode(Layout L, const BlockInfo *__r
     uint32_t sym[kSymW];
     const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
     const uint64_t obyte = blk_off[b] + bi.words_rel[s];
-    const uint32_t coff = chunk_off[(uint64_t)b * L.cpb_total + r];
+    uint64_t *st = cstat + 2 * ((uint64_t)b * L.cpb_total + r);   // this chunk's words; st[-2k]: k chunks back
     bool all8 = true;
 #pragma unroll
     for (uint32_t u = 0; u < 256 / kEncT; u++) {
@@ -436,12 +399,64 @@ __global__ __launch_bounds__(kEncT) void k_encode(Layout L, const BlockInfo *__r
         all8 = all8 && ltv[u] == 8;
     }
     // all 256 symbols with 8-bit codes (the chars of random data): the code stream is a
-    // byte substitution at a byte-aligned offset
+    // byte substitution
     const bool byte8 = __syncthreads_and(all8) != 0;
+    // ---- this chunk's bit count and this lane's bit offset in it
+    uint32_t nb = 0;
+    if (byte8) nb = 8 * n;
+    else
+        for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
+    const uint32_t inc = wave_incl_scan(nb);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    uint32_t tb = inc - nb, T = 0;
+    for (uint32_t q = 0; q < kW; q++) {
+        if (q < wv) tb += red[q];
+        T += red[q];
+    }
+    if (T == 0) return;   // one symbol in the stream: no code bits (W = 0)
+    // ---- decoupled look-back (wave 0): the stream's bits before this chunk
+    if (wv == 0) {
+        uint32_t excl = 0;
+        if (c == 0) {
+            if (lane == 0) __hip_atomic_store(st, st_word(kStInc, T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(st, st_word(kStAgg, T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t back = 1;   // lane i reads the chunk back + i places back
+            for (;;) {
+                const bool have = back + lane <= c;
+                const uint64_t v = have ? __hip_atomic_load(st - 2 * (back + lane), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                        : kStInc;   // before the stream: an inclusive 0
+                const uint64_t rdy = __ballot((v >> 62) != 0), incm = __ballot((v >> 62) == 2);
+                const uint32_t fnr = ~rdy ? (uint32_t)__builtin_ctzll(~rdy) : 64u;   // first lane not ready
+                const uint32_t fin = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;   // first inclusive prefix
+                const uint32_t upto = fin < fnr ? fin + 1 : fnr;   // lanes whose counts are summed now
+                excl += wave_sum_u32(lane < upto ? (uint32_t)v & 0x3FFFFFFFu : 0u);
+                if (fin < fnr) break;
+                back += fnr;   // (fnr == 0: the previous chunk has not published yet; poll again)
+            }
+            if (lane == 0) __hip_atomic_store(st, st_word(kStInc, excl + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_pre = excl;
+    }
+    __syncthreads();
+    const uint64_t g0 = 8 * obyte + s_pre;   // first bit of this chunk in the output
+    const uint32_t sh0 = (uint32_t)(g0 & 31);
+    // the word the previous chunk ends in is this chunk's to write: its low sh0 bits are the
+    // previous chunk's last ones, merged in last (the record's header bytes, written later, for
+    // a stream's first chunk)
+    const bool merge = c > 0 && sh0 != 0;
+    const uint32_t nw = (sh0 + T + 31) >> 5;
+    // the last word: this chunk's to write only when it ends on a word boundary (else the next
+    // chunk writes it, merged); the stream's last chunk writes through the end of the stream's
+    // W code words (zero bits past its codes, 849-928: W = ceil(bits / 32))
+    const uint32_t nst = lastc ? (uint32_t)(((8 * obyte + 32ull * bi.nwords[s] - 1) >> 5) - (g0 >> 5) + 1)
+                               : (((sh0 + T) & 31) == 0 ? nw : nw - 1);
+    uint32_t *o32 = (uint32_t *)out + (g0 >> 5);
+    uint32_t w0v = 0;   // (thread 0) the first staged word, kept for the merge
     if (byte8) {
-        const uint64_t g0 = 8 * obyte + coff;
-        const uint32_t sh0 = (uint32_t)(g0 & 31), nw = (sh0 + 8 * (c1 - c0) + 31) >> 5;
-        for (uint32_t x = tid; x < nw; x += kEncT) ws[x] = 0;
+        for (uint32_t x = tid; x < nw; x += kEncT) ws[x] = 0u;
         uint32_t v[kSymW + 1];
 #pragma unroll
         for (uint32_t q = 0; q < kSymW; q++) {
@@ -467,38 +482,21 @@ __global__ __launch_bounds__(kEncT) void k_encode(Layout L, const BlockInfo *__r
             }
         }
         __syncthreads();
-        uint32_t *o32 = (uint32_t *)out + (g0 >> 5);
-        for (uint32_t x = tid; x < nw; x += kEncT) {
-            const uint32_t val = ws[x];
-            if (x == 0 || x == nw - 1) { if (val) atomicOr(&o32[x], val); }
-            else o32[x] = val;
-        }
+        if (!lastc && tid == 0) publish_tail(st, ws, sh0 + T);
+        for (uint32_t x = (merge ? 1 : 0) + tid; x < nst; x += kEncT) o32[x] = x < nw ? ws[x] : 0u;
+        if (merge && tid == 0) merge_head(st, o32, ws[0], sh0);
         return;
     }
-    uint32_t nb = 0;
-    for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
-    // block exclusive scan of nb
-    const uint32_t inc = wave_incl_scan(nb);
-    if (lane == 63) red[wv] = inc;
-    __syncthreads();
-    uint32_t pre = 0, ctot = 0;
-    for (uint32_t q = 0; q < kW; q++) {
-        if (q < wv) pre += red[q];
-        ctot += red[q];
-    }
-    const uint32_t tb = pre + inc - nb;
-    const uint64_t g0 = 8 * obyte + coff;
-    const uint64_t gw = g0 >> 5;
-    const uint32_t sh0 = (uint32_t)(g0 & 31);
-    const uint32_t nw = (sh0 + ctot + 31) >> 5;
     // this lane's codes cover bits [p0, p1) of the staging words; whole words inside
     // that range are this lane's alone (plain LDS stores), the two end words are shared.
     // Windows of kEncWords words: a lane writes the words of its range inside the window.
     const uint32_t p0 = sh0 + tb, p1 = p0 + nb;
-    uint32_t *o32 = (uint32_t *)out + gw;
+    uint32_t prevlast = 0;   // the previous window's last word (a tail may straddle two windows)
     for (uint32_t wb = 0; wb < nw; wb += kEncWords) {
         const uint32_t we = min(nw, wb + kEncWords);
-        for (uint32_t x = tid; x < we - wb; x += kEncT) ws[x] = 0;
+        if (wb) prevlast = ws[kEncWords - 1];
+        __syncthreads();
+        for (uint32_t x = tid; x < we - wb; x += kEncT) ws[x] = 0u;
         __syncthreads();
         if (nb && (p0 >> 5) < we && ((p1 - 1) >> 5) >= wb) {
             uint32_t wi = p0 >> 5, ap = p0 & 31;
@@ -521,13 +519,18 @@ __global__ __launch_bounds__(kEncT) void k_encode(Layout L, const BlockInfo *__r
             if (ap && wi >= wb && wi < we) atomicOr(&ws[wi - wb], (uint32_t)acc);
         }
         __syncthreads();
-        for (uint32_t x = wb + tid; x < we; x += kEncT) {
-            const uint32_t v = ws[x - wb];
-            if (x == 0 || x == nw - 1) { if (v) atomicOr(&o32[x], v); }
-            else o32[x] = v;
+        if (tid == 0 && wb == 0) w0v = ws[0];
+        if (!lastc && tid == 0 && we == nw) {   // the window holding the chunk's end: publish its last bits
+            const uint32_t e = sh0 + T - 32 * wb;   // end bit inside this window
+            if (e >= 32) publish_tail(st, ws, e);
+            else __hip_atomic_store(st + 1, kStTail | (((uint64_t)ws[0] << 32 | prevlast) >> e), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
         }
+        for (uint32_t x = wb + (wb == 0 && merge ? 1 : 0) + tid; x < min(we, nst); x += kEncT) o32[x] = ws[x - wb];
         __syncthreads();
     }
+    for (uint32_t x = nw + tid; x < nst; x += kEncT) o32[x] = 0u;   // (the last chunk's zero tail)
+    if (merge && tid == 0) merge_head(st, o32, w0v, sh0);
 }
 
 __device__ inline void put_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t lane) {
@@ -564,14 +567,14 @@ __global__ __launch_bounds__(64) void k_headers(const BlockInfo *__restrict__ bi
 
 // ---------------------------------------------------------------------------
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
-                    uint32_t *hist, uint32_t *ctab, uint8_t *ltab, uint8_t *hhdr, uint32_t *chunk_off,
-                    uint64_t *blk_off, uint64_t *total, uint8_t *out, uint64_t cap, uint32_t *err, hipStream_t st,
-                    hipEvent_t *ev, hipEvent_t wait_scan, hipEvent_t rec_scan) {
+                    const uint16_t *thist, const uint32_t *bhist, const uint32_t *tile_off, uint32_t *ctab,
+                    uint8_t *ltab, uint8_t *hhdr, uint64_t *cstat, uint64_t *blk_off, uint64_t *total, uint8_t *out,
+                    uint64_t cap, uint32_t *err, hipStream_t st, hipEvent_t *ev, hipEvent_t wait_scan,
+                    hipEvent_t rec_scan) {
     const uint32_t nchunks = L.nblocks * L.cpb_total;
-    hipLaunchKernelGGL(k_hist, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, hist);
-    if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, hist, binfo, ctab, ltab, hhdr,
-                       chunk_off, err);
+    if (ev) (void)hipEventRecord(ev[0], st);   // (the histograms are k_emit's: no stage of their own)
+    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, bhist, tile_off, s0, s2, s3,
+                       binfo, ctab, ltab, hhdr, cstat, err);
     if (ev) (void)hipEventRecord(ev[1], st);
     hipLaunchKernelGGL(k_block_layout, dim3((L.nblocks + 63) / 64), dim3(64), 0, st, L.nblocks, binfo);
     if (ev) (void)hipEventRecord(ev[2], st);
@@ -579,10 +582,8 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, L.nblocks, binfo, blk_off, total, cap, err);
     if (rec_scan) (void)hipEventRecord(rec_scan, st);
     if (ev) (void)hipEventRecord(ev[3], st);
-    hipLaunchKernelGGL(k_zero_edges, dim3((nchunks + 255) / 256), dim3(256), 0, st, L, binfo, chunk_off, blk_off, out,
-                       err);
-    if (ev) (void)hipEventRecord(ev[4], st);
-    hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, chunk_off,
+    if (ev) (void)hipEventRecord(ev[4], st);   // (no edge zeroing: k_encode stores every word whole)
+    hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, cstat,
                        blk_off, out, err);
     if (ev) (void)hipEventRecord(ev[5], st);
     hipLaunchKernelGGL(k_headers, dim3(L.nblocks), dim3(64), 0, st, binfo, s0, L.sstride[0], hhdr, blk_off, out, err);

@@ -94,7 +94,9 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
                                          uint32_t *s_unknown, uint32_t *mx, uint64_t *mbx, uint32_t q0, uint32_t npos,
                                          uint32_t nload, uint32_t ilen, uint32_t w0, uint32_t dbg_in, uint16_t *dist,
                                          uint32_t rt_cap) {
-    const uint32_t dbg = kDev ? dbg_in : 0u;   // development bits exist only in k_match<true>
+    const uint32_t dbg = kDev ? uni(dbg_in) : 0u;   // development bits exist only in k_match<true>
+    q0 = uni(q0); npos = uni(npos); nload = uni(nload); ilen = uni(ilen); w0 = uni(w0);   // (arguments arrive
+    rt_cap = uni(rt_cap);                                                                 //  in VGPRs)
     const uint32_t tid = threadIdx.x;
     uint32_t *rbm = region + kTile / 2;                       // boundary bitmap, kRunBmWords
     uint16_t *prc = (uint16_t *)(rbm + kRunBmWords);          // prefix counts per bitmap word
@@ -282,20 +284,21 @@ __device__ inline uint32_t run_match_wave(const FCX_LDS uint32_t *bm, const FCX_
     if (w0 + x == 0 || ilen - x < 4) return 0u;
     const uint32_t cap = min(kMaxL, ilen - x) - 1;
     const uint32_t xlo = max(w0 + x, kWin) - kWin - w0;
-    const uint32_t ko = run_rank(bm, prc, x) - 1, klo = run_rank(bm, prc, xlo) - 1;
+    // (x is wave-uniform and so is everything derived from it: scalar registers, scalar branches)
+    const uint32_t ko = uni(run_rank(bm, prc, x) - 1), klo = uni(run_rank(bm, prc, xlo) - 1);   // one round of loads
     if (ko - klo > kRunBudget) return kUnknown;
-    const uint32_t own = rt[ko], vb0 = rt[ko + 1];
+    // second round: the own run and the run after it (the query side of ext), and each lane's
+    // candidate run with the two after it, all issued together (clamped indices, no branch);
+    // the first step of the ext walk needs nothing more
+    const uint32_t own = uni(rt[ko]), vb0 = uni(rt[ko + 1]), vb1 = uni(rt[ko + 2]);
     const uint32_t c = own >> 16, r = (vb0 & 0xFFFFu) - x;
     const bool big = r > cap;
     uint32_t best = 0;
     for (uint32_t k0 = klo; k0 < ko; k0 += 64) {
-        const uint32_t kc = k0 + lane;
-        if (kc >= ko) continue;
-        const uint32_t v = rt[kc];
-        if ((v >> 16) != c) continue;
-        const uint32_t nv = rt[kc + 1];
+        const uint32_t kc = min(k0 + lane, ko);
+        const uint32_t v = rt[kc], nv = rt[kc + 1], nnv = rt[kc + 2];
         const uint32_t sp = max(v & 0xFFFFu, xlo), ep = nv & 0xFFFFu;
-        if (ep <= xlo) continue;
+        if (k0 + lane >= ko || (v >> 16) != c || ep <= xlo) continue;
         const uint32_t A = ep - sp;
         uint32_t Lc, j = sp;
         if (big) Lc = min(A, cap);
@@ -304,16 +307,21 @@ __device__ inline uint32_t run_match_wave(const FCX_LDS uint32_t *bm, const FCX_
             // ext at run granularity (equal (byte, length) runs extend it, the first length
             // mismatch adds the shorter length); the query side meets the image end only past the cap
             uint32_t ext = 0;
-            if (r < cap) {
+            if (r < cap && (nv >> 16) == (vb0 >> 16)) {
                 const uint32_t lim = cap - r;
-                uint32_t ka = kc + 1, kb = ko + 1, va = nv, vb = vb0;
-                while ((va >> 16) == (vb >> 16)) {
-                    const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
-                    const uint32_t la = (na & 0xFFFFu) - (va & 0xFFFFu), lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
-                    if (la != lb) { ext += min(la, lb); break; }
-                    ext += la;
-                    if (ext >= lim) break;
-                    ka++; kb++; va = na; vb = nb;
+                uint32_t la = (nnv & 0xFFFFu) - (nv & 0xFFFFu), lb = (vb1 & 0xFFFFu) - (vb0 & 0xFFFFu);
+                if (la != lb) ext = min(la, lb);
+                else {   // rare: a whole run of equal byte and length, keep walking
+                    ext = la;
+                    uint32_t ka = kc + 2, kb = ko + 2, va = nnv, vb = vb1;
+                    while (ext < lim && (va >> 16) == (vb >> 16)) {
+                        const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
+                        la = (na & 0xFFFFu) - (va & 0xFFFFu);
+                        lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
+                        if (la != lb) { ext += min(la, lb); break; }
+                        ext += la;
+                        ka++; kb++; va = na; vb = nb;
+                    }
                 }
                 ext = min(ext, lim);
             }
@@ -329,25 +337,14 @@ __device__ inline uint32_t run_match_wave(const FCX_LDS uint32_t *bm, const FCX_
     return L >= kMinL ? m_pack(L, x - (8191u - (best & 0x1FFFu))) : 0u;
 }
 
-// The speculative chain of a run-mode tile from t0, evaluating m where the walks need it
-// (positions below kRmSpan were evaluated by dense_phase).  All eight waves work in parallel:
-//   A1  wave w walks its 512-position sub-tile from the sub-tile's first position (chain marked
-//       in onA; exit X1_w);
-//   A2  fix-up rounds: wave w walks from the exit of sub-tile w - 1 until it meets its own A1
-//       chain (greedy chains resynchronise within a token or two) -- from there on the A1 chain
-//       is the true one and the exit stays X1_w; a walk that never meets changes the exit, and
-//       the next round re-walks the following sub-tiles (rounds until no exit changes);
-//   C   every wave turns its sub-tile's chain (walked positions before the meeting point, the A1
-//       chain from it) into chain words, counts, prefix counts (block scan) and its part of the
-//       compact match list.
-// Past kRmSpan the mbits words are exact on chain positions and "unknown" elsewhere (no m rows
-// there: the stitch evaluates such positions itself if its walk ever reaches one).  Sets
-// *s_unknown when a window holds too many runs (the caller then publishes a lazy tile).
 // step (L + 1) of tile position x, evaluated over the run table when dense_phase / an earlier
 // walk did not (then stored with its distance); wave-uniform; 0 = unknown
 __device__ inline uint32_t rm_stepat(FCX_LDS uint32_t *region, uint32_t x, uint32_t q0, uint32_t ilen, uint32_t w0) {
     FCX_LDS uint16_t *step = (FCX_LDS uint16_t *)region;
-    uint32_t sv = step[x];
+    // below the span dense_phase stored every position; past it a walk meets only positions
+    // no walk has evaluated (A1 walks its own sub-tile forward, A2 stops at the A1 chain), so
+    // the lookup would only add a round trip: evaluate directly
+    uint32_t sv = x < kRmSpan ? uni(step[x]) : 0u;
     if (sv == 0) {
         const FCX_LDS uint32_t *rbm = region + kTile / 2;
         const uint32_t mm = run_match_wave(rbm, (const FCX_LDS uint16_t *)(rbm + kRunBmWords), region + kRunTableOff,
@@ -365,7 +362,8 @@ __device__ inline uint32_t rm_stepat(FCX_LDS uint32_t *region, uint32_t x, uint3
 __device__ __noinline__ void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32_t *s_ex, FCX_LDS uint32_t *s_unknown,
                                         uint32_t q0, uint32_t nt, uint32_t ilen, uint32_t w0, uint32_t t0, uint64_t *mbw,
                                         uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t *mt, uint32_t dbg) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);   // walks: wave-uniform, scalar
+    q0 = uni(q0); nt = uni(nt); ilen = uni(ilen); w0 = uni(w0); t0 = uni(t0);   // (arguments arrive in VGPRs)
     FCX_LDS uint16_t *step = (FCX_LDS uint16_t *)region;
     FCX_LDS uint16_t *dist = (FCX_LDS uint16_t *)(region + kRmDist);
     FCX_LDS uint32_t *onA = region + kRmOnA, *onB = region + kRmOnB;
@@ -387,10 +385,10 @@ __device__ __noinline__ void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32
         if (lost && lane == 0) *s_unknown = 1;
     }
     __syncthreads();
-    if (*s_unknown || (dbg & (1u << 18))) return;   // (timing: A1 only)
+    if (uni(*s_unknown) || (dbg & (1u << 18))) return;   // (timing: A1 only)
     uint32_t curE = a, meet = a;   // this sub-tile's entry and where its chain joins the A1 chain
     for (uint32_t round = 0; round < kWaves; round++) {   // A2
-        const uint32_t E = wv == 0 ? 0u : s_ex[wv - 1];
+        const uint32_t E = wv == 0 ? 0u : uni(s_ex[wv - 1]);
         __syncthreads();
         bool changed = false;
         if (a < nt && E != curE) {
@@ -398,7 +396,7 @@ __device__ __noinline__ void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32
             if (lane < kRmSub / 32) onB[a / 32 + lane] = 0;
             __builtin_amdgcn_wave_barrier();
             uint32_t x = E;
-            while (x < bnd && !((onA[x >> 5] >> (x & 31)) & 1u)) {
+            while (x < bnd && !((uni(onA[x >> 5]) >> (x & 31)) & 1u)) {
                 const uint32_t sv = rm_stepat(region, x, q0, ilen, w0);
                 if (sv == 0) { lost = true; break; }
                 if (lane == 0) onB[x >> 5] |= 1u << (x & 31);
@@ -406,15 +404,15 @@ __device__ __noinline__ void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32
             }
             meet = x < bnd ? x : bnd;
             const uint32_t ex = x < bnd ? X1 : x;
-            changed = ex != s_ex[wv];
+            changed = ex != uni(s_ex[wv]);
             if (lane == 0) {
                 s_ex[wv] = ex;
                 if (lost) *s_unknown = 1;
             }
         }
-        if (__syncthreads_or(changed ? 1 : 0) == 0 || *s_unknown) break;
+        if (__syncthreads_or(changed ? 1 : 0) == 0 || uni(*s_unknown)) break;
     }
-    if (*s_unknown || (dbg & (1u << 19))) return;   // (timing: A1 + A2)
+    if (uni(*s_unknown) || (dbg & (1u << 19))) return;   // (timing: A1 + A2)
     // C: lanes 0..7 of wave w take the sub-tile's eight chain words
     const uint32_t gw = a / 64 + lane;                 // tile word of this lane
     const bool own = lane < kRmSub / 64 && 64 * gw < nt;
@@ -521,7 +519,8 @@ __device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region
                                            uint32_t *s_np, uint32_t *s_unknown, uint32_t *s_match, uint32_t *mrow,
                                            uint64_t *mbw, uint32_t q0, uint32_t npos, uint32_t ins_end, uint32_t w0,
                                            uint32_t blen, uint32_t ntile, uint32_t dbg_in) {
-    const uint32_t dbg = kDev ? dbg_in : 0u;
+    const uint32_t dbg = kDev ? uni(dbg_in) : 0u;
+    q0 = uni(q0); npos = uni(npos); ins_end = uni(ins_end); w0 = uni(w0); blen = uni(blen); ntile = uni(ntile);
     const uint32_t tid = threadIdx.x;
     const uint32_t kw[4] = {kw0, kw1, kw2, kw3};
     auto hash_of = [&](uint32_t r) -> uint32_t {

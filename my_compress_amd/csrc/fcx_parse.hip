@@ -44,11 +44,11 @@ __device__ uint32_t lazy_match(const uint32_t *dw, uint32_t dbase, uint32_t blen
         if (xe < x && lds_key3(dw, xe) == key &&
             (best < kMinL || lds_ld1(dw, xe + best) == lds_ld1(dw, x + best)))
             Lc = lds_match_len(dw, xe, x, kMinL, cap);
-        const uint32_t mx = wave_max_u32(Lc);
-        if (mx > best) {
-            const uint64_t msk = __ballot(Lc == mx);
-            bestx = cb + (uint32_t)(__ffsll((unsigned long long)msk) - 1);
-            best = mx;
+        // the step's longest, then leftmost candidate in one DPP maximum (window positions < 2^15)
+        const uint32_t mk = wave_max_dpp(Lc ? (Lc << 15) | (32767u - xe) : 0u);
+        if ((mk >> 15) > best) {   // strict: an earlier step's candidate wins a tie (leftmost)
+            best = mk >> 15;
+            bestx = 32767u - (mk & 0x7FFFu);
         }
         if (best >= cap) break;
     }
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                                                const uint32_t *__restrict__ mtok, uint32_t *__restrict__ tile_off,
                                                uint32_t *__restrict__ tconv, BlockInfo *__restrict__ binfo,
                                                uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_p,
-                                               uint8_t *__restrict__ s_golomb) {
+                                               uint8_t *__restrict__ s_golomb, uint32_t *__restrict__ bhist) {
     __shared__ uint32_t mL[kTile];
     __shared__ uint32_t sti[64][6];          // per tile of the batch: flags, exit, totals, k_resolve verdict
     __shared__ uint32_t sfp[64][5];          // k_resolve: final counts, exit, conv record
@@ -317,6 +317,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
     const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
     const uint8_t *d = in + bstart;
     const uint32_t ntiles = (blen + kTile - 1) / kTile;
+    for (uint32_t x = lane; x < kStreams * 256; x += 64) bhist[(uint64_t)b * kStreams * 256 + x] = 0;   // k_emit's bins
     uint32_t e = 0, dbase = 0xFFFFFFFFu, nlazy = 0, lazy_tiles = 0;
     Cnt3 run{0, 0, 0};
     uint4 pv[kTile / 256];   // prefetched rows / mbits / chain word of tile pk
@@ -674,6 +675,35 @@ __device__ void emit_literal_tile(const uint32_t *lin, uint32_t nt, uint32_t tok
     }
 }
 
+// ---- symbol histograms of the block's four Huffman sub-streams, built here while each tile's
+// stream bits are still in LDS (my_huffman_encode_char's count, my_compress.cpp:998-1000):
+// the tile counts its chars (one byte per token) and the flag / distance / golomb bytes that lie
+// wholly inside its bits; a byte that straddles two tiles' bits (or the stream's zero tail) is
+// k_tree's, read back from the finished stream.  Chars go out as the tile's row of u16 counts
+// (one plain 512-B store), the other three streams by atomics into the block's bins (few bins
+// per tile on random data).
+__device__ inline void hist_inside(const uint32_t *w, uint64_t b0, uint64_t b1, uint32_t *h, uint32_t tid) {
+    const uint64_t wbase = b0 >> 5;   // staged word 0 = global word b0 >> 5
+    const uint64_t k0 = (b0 + 7) >> 3, k1 = b1 >> 3;
+    for (uint64_t k = k0 + tid; k < k1; k += 256)
+        atomicAdd(&h[(w[(k >> 2) - wbase] >> (8 * (k & 3))) & 0xFFu], 1u);
+}
+__device__ inline void hist_bytes16(const uint32_t in4[4], uint32_t n, uint32_t *h) {   // the first n of 16 bytes
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++)
+        if (q < n) atomicAdd(&h[(in4[q >> 2] >> (8 * (q & 3))) & 0xFFu], 1u);
+}
+// after a barrier: the tile's chars row and the block bins of the other streams
+__device__ inline void hist_flush(const uint32_t (*hh)[256], uint16_t *trow, uint32_t *bh, uint32_t tid) {
+    trow[tid] = (uint16_t)hh[1][tid];
+#pragma unroll
+    for (uint32_t q = 0; q < 3; q++) {
+        const uint32_t st = q == 0 ? 0u : q + 1;
+        const uint32_t v = hh[st][tid];
+        if (v) atomicAdd(&bh[st * 256 + tid], v);
+    }
+}
+
 constexpr uint32_t kInW = (kTile + kLookAhead) / 4 + 2;   // tile input + look-ahead (dwords)
 
 // Latency shape: every load that does not depend on another goes out first (tile
@@ -685,8 +715,10 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
                                               const BlockInfo *__restrict__ binfo, const uint32_t *__restrict__ mtok,
                                               const uint32_t *__restrict__ tconv, const uint32_t *__restrict__ tinfo,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
-                                              uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb) {
+                                              uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb,
+                                              uint16_t *__restrict__ thist, uint32_t *__restrict__ bhist) {
     __shared__ uint32_t sh[16];
+    __shared__ uint32_t hh[kStreams][256];   // this tile's symbol counts per stream
     __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW], lc[kCharW];
     __shared__ uint32_t lin[kInW];           // input bytes [t0, t0 + kTile + kLookAhead) of the block
     __shared__ uint32_t lmt[kTileMatches];   // the tile's compact match list from its conv point
@@ -698,6 +730,9 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     if (t0 >= blen) return;
     const uint32_t t1 = min(blen, t0 + kTile);
     const uint32_t tix = blockIdx.x;
+    for (uint32_t x = tid; x < kStreams * 256; x += 256) (&hh[0][0])[x] = 0;   // (every path's barriers order it)
+    uint16_t *trow = thist + (uint64_t)tix * 256;
+    uint32_t *bh = bhist + (uint64_t)b * kStreams * 256;
 
     // ---- round 1: independent loads ----
     const bool last = t1 == blen;
@@ -788,6 +823,12 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         flush_words((uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]), fw0, lf, nfw, tid);
         flush_words((uint32_t *)(s_p + (uint64_t)b * L.sstride[2]), pw0, lp, npw, tid);
         flush_words((uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]), gw0, lg, ngw, tid);
+        if (tid == 0 && tot[0]) hh[1][ub] += tot[0];   // every token's char is the tile's byte
+        hist_inside(lf, tok0, tok0 + tot[0], hh[0], tid);
+        hist_inside(lp, (uint64_t)kPBits * mi0, (uint64_t)kPBits * (mi0 + tot[1]), hh[2], tid);
+        hist_inside(lg, g0, (uint64_t)g0 + tot[2], hh[3], tid);
+        __syncthreads();
+        hist_flush(hh, trow, bh, tid);
         return;
     }
 #pragma unroll
@@ -798,6 +839,14 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         __syncthreads();
         emit_literal_tile(lin, t1 - t0, tok0, s_chars + (uint64_t)b * L.sstride[1],
                           (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]));
+        // chars = the tile's bytes; every whole flag byte is 0xFF
+        hist_bytes16(in4, s < t1 ? min(16u, t1 - s) : 0u, hh[1]);
+        if (tid == 0) {
+            const uint32_t k0 = (tok0 + 7) >> 3, k1 = (tok0 + (t1 - t0)) >> 3;
+            if (k1 > k0) hh[0][0xFF] += k1 - k0;
+        }
+        __syncthreads();
+        hist_flush(hh, trow, bh, tid);
         return;
     }
 
@@ -889,12 +938,15 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         }
         fl = 0xFFFFu;
         nt_lane = 16;
+        hist_bytes16(in4, 16, hh[1]);
     } else
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
         if ((bits >> q) & 1u) {
             const uint32_t Lm = m_len(mm[q]);
-            lcb[tokA + nt_lane - 4 * cw0] = Lm ? lb[s - t0 + q + Lm] : (uint8_t)(in4[q >> 2] >> (8 * (q & 3)));
+            const uint8_t ch = Lm ? lb[s - t0 + q + Lm] : (uint8_t)(in4[q >> 2] >> (8 * (q & 3)));
+            lcb[tokA + nt_lane - 4 * cw0] = ch;
+            atomicAdd(&hh[1][ch], 1u);
             if (Lm == 0) {
                 fl |= 1u << nt_lane;
             } else {
@@ -940,19 +992,24 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     flush_words((uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]), fw0, lf, nfw, tid);
     flush_words((uint32_t *)(s_p + (uint64_t)b * L.sstride[2]), pw0, lp, npw, tid);
     flush_words((uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]), gw0, lg, ngw, tid);
+    hist_inside(lf, tok0, tok0 + tot[0], hh[0], tid);
+    hist_inside(lp, (uint64_t)kPBits * mi0, (uint64_t)kPBits * (mi0 + tot[1]), hh[2], tid);
+    hist_inside(lg, g0, (uint64_t)g0 + tot[2], hh[3], tid);
+    __syncthreads();
+    hist_flush(hh, trow, bh, tid);
 }
 
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, hipStream_t st, hipEvent_t *ev) {
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev) {
     const uint32_t ntiles = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_resolve, dim3(ntiles), dim3(64), 0, st, L, m, mbits, chain, chain_pfx, tinfo, fp);
     hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, mtok,
-                       tile_off, tconv, binfo, s_flags, s_p, s_golomb);
+                       tile_off, tconv, binfo, s_flags, s_p, s_golomb, bhist);
     if (ev) (void)hipEventRecord(ev[0], st);
     hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok, tconv,
-                       tinfo, s_flags, s_chars, s_p, s_golomb);
+                       tinfo, s_flags, s_chars, s_p, s_golomb, thist, bhist);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 
