@@ -754,6 +754,15 @@ __device__ inline void uniform_tile_out(uint32_t *sc /* >= kMT + 1 words */, uin
     }
 }
 
+// Workgroups are dealt round-robin over the 8 XCDs (workgroups w and w + 8 share one L2).  Each
+// XCD takes a contiguous run of tiles instead, so the neighbouring tiles that re-read a tile's
+// bytes as their 2 KiB left halo run on the same XCD at about the same time and find them in
+// its L2 (a bijection of [0, n); any placement stays correct, only the re-reads move).
+__device__ inline uint32_t xcd_tile(uint32_t w, uint32_t n) {
+    const uint32_t x = w & 7u, j = w >> 3, q = n >> 3, r = n & 7u;
+    return x * q + min(x, r) + j;
+}
+
 // kDev = false is the product kernel: every development / test-mode bit is compiled out.
 // k_match<true> carries them (phase exits for tools/matchphase.py through fcx_debug_match, and
 // the forced tile modes of fcx_ctx_set_match_mode, which the parity tests use).
@@ -782,7 +791,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __shared__ uint32_t s_red[4 * kWaves];   // cross-wave scan partials (rmode_walk: exits + 3 scans)
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t b = blockIdx.x / L.tpb, k = blockIdx.x % L.tpb;
+    const uint32_t bx = xcd_tile(blockIdx.x, gridDim.x);   // this workgroup's tile
+    const uint32_t b = bx / L.tpb, k = bx % L.tpb;
     const uint64_t bstart = (uint64_t)b * L.B;
     const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
     const uint32_t t0 = k * kTile;
@@ -896,7 +906,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if (nruns_img == 1 && !(dbg & 12u)) {   // one byte value over the whole image (zeros)
             uniform_tile_out(region, s_red, mbits + (uint64_t)b * L.wpb,
                              chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64),
-                             chain_pfx + (uint64_t)blockIdx.x * (kTile / 64), tinfo + 8ull * blockIdx.x, t0, t1, blen);
+                             chain_pfx + (uint64_t)bx * (kTile / 64), tinfo + 8ull * bx, t0, t1, blen);
             return;
         }
         for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
@@ -1151,14 +1161,14 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
     if (dbg & 64u) return;   // timing: + queries (no parse)
     uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
-    uint32_t *ti = tinfo + 8ull * blockIdx.x;
+    uint32_t *ti = tinfo + 8ull * bx;
     const uint32_t nwords = (t1 - t0 + 63) / 64;
     if (rmode) {
         uint64_t *mbw = mbits + (uint64_t)b * L.wpb + (t0 >> 6);
         if (s_unknown == 0)
             rmode_walk((FCX_LDS uint32_t *)region, (FCX_LDS uint32_t *)s_red, (FCX_LDS uint32_t *)&s_unknown, q0,
                        t1 - t0, blen - w0, w0, t0, mbw, cw,
-                       chain_pfx + (uint64_t)blockIdx.x * (kTile / 64), ti, mtok + (uint64_t)blockIdx.x * kTileMatches, dbg);
+                       chain_pfx + (uint64_t)bx * (kTile / 64), ti, mtok + (uint64_t)bx * kTileMatches, dbg);
         __syncthreads();
         if (s_unknown != 0) {   // lazy tile: m rows in the span only, "unknown" past it
             for (uint32_t w = tid; w < nwords; w += kMT) {
@@ -1181,7 +1191,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if (tid < nwords) {
             const uint32_t nb = min(64u, t1 - t0 - 64 * tid);
             cw[tid] = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
-            chain_pfx[(uint64_t)blockIdx.x * (kTile / 64) + tid] = 64ull * tid;   // tokens before; no matches
+            chain_pfx[(uint64_t)bx * (kTile / 64) + tid] = 64ull * tid;   // tokens before; no matches
         }
         if (tid == 0) { ti[0] = 0; ti[1] = t1; ti[2] = t1 - t0; ti[3] = 0; ti[4] = 0; }
         return;
@@ -1189,7 +1199,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
     if (sparse && !dense && !(dbg & 65536u) &&
         sparse_parse((const uint64_t *)(region + kSpMb), step, region + kResLds, region + kSpP, t1 - t0, t0, cw,
-                     chain_pfx + (uint64_t)blockIdx.x * (kTile / 64), ti, mtok + (uint64_t)blockIdx.x * kTileMatches))
+                     chain_pfx + (uint64_t)bx * (kTile / 64), ti, mtok + (uint64_t)bx * kTileMatches))
         return;
 
     // ---- 4. tile-local greedy parse ----
@@ -1289,7 +1299,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         // from the search results); with m rows only in the first kResolveSpan
         // positions, k_emit takes the rest of the tile's matches from here
         const uint32_t *res_lds = region + kResLds;
-        uint32_t *mt = mtok + (uint64_t)blockIdx.x * kTileMatches + pre[1];
+        uint32_t *mt = mtok + (uint64_t)bx * kTileMatches + pre[1];
 #pragma unroll
         for (uint32_t q = 0; q < kSeg; q++)
             if (((T >> q) & 1u) && stp[q] > 1) *mt++ = res_lds[s - t0 + q];
@@ -1302,7 +1312,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 #pragma unroll
         for (uint32_t q = 0; q < kLanesPerWord; q++) word |= (uint64_t)Vs[tid + q] << (kSeg * q);
         cw[w] = word;
-        chain_pfx[(uint64_t)blockIdx.x * (kTile / 64) + w] =
+        chain_pfx[(uint64_t)bx * (kTile / 64) + w] =
             (uint64_t)pre[0] | ((uint64_t)pre[1] << 13) | ((uint64_t)pre[2] << 24);
     }
     if (tid == 0) {

@@ -4,8 +4,7 @@ Keys are "<leg>:<stage>" (legs rand, text, c3 = text at 256 KiB blocks, zeros, r
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch (summed over XCDs).  On gfx950 FETCH_SIZE
 tallies 128-B requests at 64 B (MI355X_MICROARCH.md §HBM), so read bytes = 2 x FETCH_SIZE
-KiB; the factor is re-checked here on k_hist, which reads its streams exactly once
-(calibration printed).  WRITE_SIZE is taken as is."""
+KiB.  WRITE_SIZE is taken as is."""
 import csv
 import collections
 import glob
@@ -22,7 +21,7 @@ for kind in names:
     for ctr in ["FETCH_SIZE", "WRITE_SIZE"]:
         for f in glob.glob(os.path.join(ROOT, f"gpurun_out/traffic_{kind}_{ctr}/run_counter_collection.csv")):
             for r in csv.DictReader(open(f)):
-                name = r["Kernel_Name"].split("(")[0].replace("fcx::", "")
+                name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("fcx::", "").split("<")[0]
                 vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for name, d in vals.items():
         if not name.startswith("k_"):
