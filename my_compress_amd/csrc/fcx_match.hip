@@ -274,69 +274,6 @@ constexpr uint32_t kRmRunCap = kRmOnA - kRunTableOff - 4;        // run table en
 constexpr uint32_t kRmSub = kTile / kWaves;                      // 512 positions per wave's sub-tile walk
 static_assert(kRmRunCap >= kRunTile + 8, "run-mode table");
 
-// exact m of image position x (block position w0 + x) over the run table, by the whole wave:
-// one window run per lane (64 per pass), each lane's best candidate in its run packed as
-// L << 13 | (8191 - j), the wave maximum = the longest, then leftmost match (the rules of
-// run_match, fcx_device.h).  ilen = block length - w0.  kUnknown: more than kRunBudget runs.
-__device__ inline uint32_t run_match_wave(const FCX_LDS uint32_t *bm, const FCX_LDS uint16_t *prc,
-                                          const FCX_LDS uint32_t *rt, uint32_t x, uint32_t ilen, uint32_t w0) {
-    const uint32_t lane = lane_id();
-    if (w0 + x == 0 || ilen - x < 4) return 0u;
-    const uint32_t cap = min(kMaxL, ilen - x) - 1;
-    const uint32_t xlo = max(w0 + x, kWin) - kWin - w0;
-    // (x is wave-uniform and so is everything derived from it: scalar registers, scalar branches)
-    const uint32_t ko = uni(run_rank(bm, prc, x) - 1), klo = uni(run_rank(bm, prc, xlo) - 1);   // one round of loads
-    if (ko - klo > kRunBudget) return kUnknown;
-    // second round: the own run and the run after it (the query side of ext), and each lane's
-    // candidate run with the two after it, all issued together (clamped indices, no branch);
-    // the first step of the ext walk needs nothing more
-    const uint32_t own = uni(rt[ko]), vb0 = uni(rt[ko + 1]), vb1 = uni(rt[ko + 2]);
-    const uint32_t c = own >> 16, r = (vb0 & 0xFFFFu) - x;
-    const bool big = r > cap;
-    uint32_t best = 0;
-    for (uint32_t k0 = klo; k0 < ko; k0 += 64) {
-        const uint32_t kc = min(k0 + lane, ko);
-        const uint32_t v = rt[kc], nv = rt[kc + 1], nnv = rt[kc + 2];
-        const uint32_t sp = max(v & 0xFFFFu, xlo), ep = nv & 0xFFFFu;
-        if (k0 + lane >= ko || (v >> 16) != c || ep <= xlo) continue;
-        const uint32_t A = ep - sp;
-        uint32_t Lc, j = sp;
-        if (big) Lc = min(A, cap);
-        else if (A < r) Lc = A;
-        else {
-            // ext at run granularity (equal (byte, length) runs extend it, the first length
-            // mismatch adds the shorter length); the query side meets the image end only past the cap
-            uint32_t ext = 0;
-            if (r < cap && (nv >> 16) == (vb0 >> 16)) {
-                const uint32_t lim = cap - r;
-                uint32_t la = (nnv & 0xFFFFu) - (nv & 0xFFFFu), lb = (vb1 & 0xFFFFu) - (vb0 & 0xFFFFu);
-                if (la != lb) ext = min(la, lb);
-                else {   // rare: a whole run of equal byte and length, keep walking
-                    ext = la;
-                    uint32_t ka = kc + 2, kb = ko + 2, va = nnv, vb = vb1;
-                    while (ext < lim && (va >> 16) == (vb >> 16)) {
-                        const uint32_t na = rt[ka + 1], nb = rt[kb + 1];
-                        la = (na & 0xFFFFu) - (va & 0xFFFFu);
-                        lb = (nb & 0xFFFFu) - (vb & 0xFFFFu);
-                        if (la != lb) { ext += min(la, lb); break; }
-                        ext += la;
-                        ka++; kb++; va = na; vb = nb;
-                    }
-                }
-                ext = min(ext, lim);
-            }
-            Lc = min(r + ext, cap);
-            if (ext) j = ep - r;
-        }
-        best = max(best, (Lc << 13) | (8191u - j));
-    }
-    const uint32_t sp = max(own & 0xFFFFu, xlo);   // candidates inside the own run give r
-    if (sp < x) best = max(best, ((big ? cap : r) << 13) | (8191u - sp));
-    best = wave_max_dpp(best);
-    const uint32_t L = best >> 13;
-    return L >= kMinL ? m_pack(L, x - (8191u - (best & 0x1FFFu))) : 0u;
-}
-
 // step (L + 1) of tile position x, evaluated over the run table when dense_phase / an earlier
 // walk did not (then stored with its distance); wave-uniform; 0 = unknown
 __device__ inline uint32_t rm_stepat(FCX_LDS uint32_t *region, uint32_t x, uint32_t q0, uint32_t ilen, uint32_t w0) {

@@ -55,6 +55,52 @@ __device__ uint32_t lazy_match(const uint32_t *dw, uint32_t dbase, uint32_t blen
     return best >= kMinL ? m_pack(best, x - bestx) : 0u;
 }
 
+// Exact m of block position t for the stitch over a run table of its window [t - 2047, t + 258),
+// built from the staged bytes dw (dw byte 0 = block position dbase): the run decomposition gives
+// the leftmost-longest match in closed form (run_match, fcx_device.h), evaluated by the wave
+// (run_match_wave) -- a few thousand cycles where the byte-by-byte window search (lazy_match)
+// spends 10^5 on long-run data.  kUnknown when the window holds more runs than the table holds
+// or than kRunBudget: the caller then searches byte by byte.
+constexpr uint32_t kStRunCap = 1020;                        // run table entries (window runs + sentinel)
+constexpr uint32_t kStBmWords = (kWin + kMaxL + 1) / 32 + 2;   // boundary bits 0 .. 2305
+__device__ uint32_t stitch_run_match(const uint32_t *dw, uint32_t dbase, uint32_t blen, uint32_t t,
+                                     FCX_LDS uint32_t *bm, FCX_LDS uint16_t *prc, FCX_LDS uint32_t *rt) {
+    const uint32_t lane = lane_id();
+    dbase = uni(dbase); blen = uni(blen); t = uni(t);
+    const uint32_t lo = t > kWin ? t - kWin : 0;          // image position 0 = block position lo
+    const uint32_t n = min(t + kMaxL, blen) - lo;         // image bytes (a match from t stays inside)
+    const uint32_t ib = lo - dbase;                       // dw byte of image position 0
+    for (uint32_t y0 = 0; y0 <= n; y0 += 64) {            // boundary bitmap by ballot; sentinel bit at n
+        const uint32_t y = y0 + lane;
+        const bool bit = y == n || (y < n && (y == 0 || lds_ld1(dw, ib + y) != lds_ld1(dw, ib + y - 1)));
+        const uint64_t bal = __ballot(bit);
+        if (lane == 0) { bm[y0 >> 5] = (uint32_t)bal; bm[(y0 >> 5) + 1] = (uint32_t)(bal >> 32); }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nw = (n >> 5) + 1;                     // words holding bits 0 .. n
+    const uint32_t c0 = lane < nw ? (uint32_t)__builtin_popcount(bm[lane]) : 0u;
+    const uint32_t c1 = lane + 64 < nw ? (uint32_t)__builtin_popcount(bm[lane + 64]) : 0u;
+    const uint32_t i0 = wave_incl_scan(c0), i1 = wave_incl_scan(c1);
+    const uint32_t t0s = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
+    const uint32_t nruns = t0s + (uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
+    if (nruns > kStRunCap) return kUnknown;
+    const uint32_t p0 = i0 - c0, p1 = t0s + i1 - c1;
+    if (lane < nw) prc[lane] = (uint16_t)p0;
+    if (lane + 64 < nw) prc[lane + 64] = (uint16_t)p1;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {                    // run table: start | byte << 16 (sentinel 0x100)
+        const uint32_t w = lane + 64 * h;
+        if (w >= nw) continue;
+        uint32_t o = h ? p1 : p0;
+        for (uint32_t v = bm[w]; v; v &= v - 1, o++) {
+            const uint32_t y = 32 * w + (uint32_t)__builtin_ctz(v);
+            rt[o] = y | (y < n ? lds_ld1(dw, ib + y) << 16 : 0x1000000u);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return run_match_wave(bm, prc, rt, t - lo, blen - lo, lo);
+}
+
 // stage block bytes [dbase, dbase + kLazyWindow) into dw (zero padded)
 __device__ void load_window(uint32_t *dw, const uint8_t *d, uint32_t dbase, uint32_t blen) {
     const uint32_t lane = lane_id();
@@ -310,6 +356,8 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
     __shared__ uint64_t bmL[kTile / 64];
     __shared__ uint64_t mbL[kTile / 64];
     __shared__ uint32_t dw[kLazyWindow / 4 + 4];
+    __shared__ uint32_t srm_bm[kStBmWords], srm_rt[kStRunCap + 4];   // stitch_run_match's run table
+    __shared__ uint16_t srm_prc[kStBmWords];
 
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
@@ -546,7 +594,9 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                     load_window(dw, d, dbase, blen);
                     __syncthreads();
                 }
-                mm = lazy_match(dw, dbase, blen, t);
+                mm = stitch_run_match(dw, dbase, blen, t, (FCX_LDS uint32_t *)srm_bm, (FCX_LDS uint16_t *)srm_prc,
+                                      (FCX_LDS uint32_t *)srm_rt);
+                if (mm == kUnknown) mm = lazy_match(dw, dbase, blen, t);
                 nlazy++;
                 if (lane == 0) m[bstart + t] = mm;
             }
