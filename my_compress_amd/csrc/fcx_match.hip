@@ -68,6 +68,12 @@ constexpr uint32_t kRegionWords = kBucketWords > kFilterWords ? kBucketWords : k
 constexpr uint32_t kResLds = kRegionWords - kTile;   // search results (m) per tile position, kept for the
                                                      // compact match list; clear of step and the parse scratch
 static_assert(kResLds >= kTile / 2 + 3 * kMT + 1, "results clear of step and the parse scratch");
+// bucket scan pass B (bucket search only): each wave's hot-query slots and owner marks, in the
+// region words the counters and entries leave free
+constexpr uint32_t kHotCap = 32;                                   // hot queries per wave and group
+constexpr uint32_t kHotWords = 3 * kHotCap + 16;                   // x, base, best per slot + 64 u8 marks
+constexpr uint32_t kScanHot = kHeadWords + kEntWords;
+static_assert(kScanHot + kHotWords * kWaves <= kRegionWords, "hot-query scratch inside the region");
 // dense-window phase (run table) inside the same region
 constexpr uint32_t kRunBmWords = 208;                // 6656 bitmap positions >= kTileBytes + 1, 13 x kMT
 constexpr uint32_t kRunListWords = 2 * 64 * kWaves;   // per-wave candidate lists (se, ext)
@@ -90,10 +96,11 @@ __device__ inline uint32_t lanes_below(uint64_t m) {
 // block length - image base, w0 = image base in the block.  mbx (whole-tile mode,
 // no bucket search ran): mbits of image position 0, written here per 64 positions.
 template <bool kDev>
-__device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, uint16_t *step, uint32_t *s_red,
-                                         uint32_t *s_unknown, uint32_t *mx, uint64_t *mbx, uint32_t q0, uint32_t npos,
-                                         uint32_t nload, uint32_t ilen, uint32_t w0, uint32_t dbg_in, uint16_t *dist,
-                                         uint32_t rt_cap) {
+__device__ __attribute__((always_inline)) inline void dense_phase_body(const uint32_t *sdw, uint32_t *region, uint16_t *step,
+                                                                      uint32_t *s_red, uint32_t *s_unknown, uint32_t *mx,
+                                                                      uint64_t *mbx, uint32_t q0, uint32_t npos, uint32_t nload,
+                                                                      uint32_t ilen, uint32_t w0, uint32_t dbg_in,
+                                                                      uint16_t *dist, uint32_t rt_cap) {
     const uint32_t dbg = kDev ? uni(dbg_in) : 0u;   // development bits exist only in k_match<true>
     q0 = uni(q0); npos = uni(npos); nload = uni(nload); ilen = uni(ilen); w0 = uni(w0);   // (arguments arrive
     rt_cap = uni(rt_cap);                                                                 //  in VGPRs)
@@ -260,6 +267,15 @@ __device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, 
     }
     if (left) *s_unknown = 1;
     __syncthreads();
+}
+// the search kernel's copy (tiles the bucket search left unknown positions in): out of line, so its
+// registers do not weigh on the search; the run-mode kernel inlines the body
+template <bool kDev>
+__device__ __noinline__ void dense_phase(const uint32_t *sdw, uint32_t *region, uint16_t *step, uint32_t *s_red,
+                                         uint32_t *s_unknown, uint32_t *mx, uint64_t *mbx, uint32_t q0, uint32_t npos,
+                                         uint32_t nload, uint32_t ilen, uint32_t w0, uint32_t dbg_in, uint16_t *dist,
+                                         uint32_t rt_cap) {
+    dense_phase_body<kDev>(sdw, region, step, s_red, s_unknown, mx, mbx, q0, npos, nload, ilen, w0, dbg_in, dist, rt_cap);
 }
 
 // ---- 3c. run-mode tiles (whole-tile run table: zeros-free low-entropy data, e.g. runs).
@@ -907,15 +923,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // the entries of slabs <= s (every later entry lies right of x).  The query scans only
     // between the two snapshots: about half of its bucket.
     uint32_t ins_hr[kIns];                                             // bucket << 16 | tag << 13 | rank
-    // queries 0..3: lo rank | hi rank << 16 (hi 0xFFFF = bucket end); queries 4..7 (live
-    // through the first group's search: two registers) keep only their lo rank, the bound
-    // that prunes most there, two u16 per register
-    uint32_t snap[kQPL / 2], slo[kQPL / 4];
+    // query r: lo rank | hi rank << 16 (hi 0xFFFF = bucket end)
+    uint32_t snap[kQPL];
     const uint32_t qsl = q0 >> 9;   // slab of query r = r + qsl (q0 = 0 or 2048)
 #pragma unroll
-    for (uint32_t r = 0; r < kQPL / 2; r++) snap[r] = 0xFFFF0000u;
-#pragma unroll
-    for (uint32_t r = 0; r < kQPL / 4; r++) slo[r] = 0u;
+    for (uint32_t r = 0; r < kQPL; r++) snap[r] = 0xFFFF0000u;
     auto qbucket = [&](uint32_t r) -> uint32_t {   // bucket of query r (its insertion record)
         return (qsl ? ins_hr[r + 4] : ins_hr[r]) >> 16;
     };
@@ -937,12 +949,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             // lo: the query is not inserted yet; its bucket comes from its key
             if ((qsl == 4 && p + 1 == r) || (qsl == 0 && p + 5 == r)) {
                 const uint32_t bk = key_mix(lds_key3(sdw, q0 + tid + kMT * r)) >> (24 - kHashBits);
-                if (r < kQPL / 2) snap[r % (kQPL / 2)] = (snap[r % (kQPL / 2)] & 0xFFFF0000u) | counter(bk);
-                else slo[(r - kQPL / 2) >> 1] |= counter(bk) << (16 * (r & 1));
+                snap[r] = (snap[r] & 0xFFFF0000u) | counter(bk);
             }
-            if (r < kQPL / 2 && ((qsl == 4 && p == r + 5) || (qsl == 0 && p == r + 1))) {
+            if ((qsl == 4 && p == r + 5) || (qsl == 0 && p == r + 1)) {
                 const uint32_t bk = qbucket(r);
-                if (bk != 0xFFFFu) snap[r % (kQPL / 2)] = (snap[r % (kQPL / 2)] & 0xFFFFu) | (counter(bk) << 16);
+                if (bk != 0xFFFFu) snap[r] = (snap[r] & 0xFFFFu) | (counter(bk) << 16);
             }
         }
         __syncthreads();
@@ -978,9 +989,23 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
     if (dbg & 32u) return;   // timing: + counting sort
     // ---- 3. queries: position i = w0 + q0 + tid + kMT*r, kIlp at a time ----
+    // Pass A: every lane walks its kIlp queries' bucket ranges together (independent LDS
+    // loads), but only for their first K entries.  K is the smallest count that leaves at most
+    // kHotCap queries of the wave with entries beyond it, so a few hot keys (text: " th",
+    // "the") no longer hold all 64 lanes for their whole range.  Pass B deals the hot queries'
+    // remaining (query, entry) pairs over the wave, 64 at a time, one per lane: a pair finds
+    // its query through owner marks (the hot slot whose segment starts in the chunk marks it; a
+    // running maximum carries the marks along), and its candidate length goes into the slot by
+    // an LDS atomic maximum of L << 13 | (8191 - position) (longest, then leftmost; the slot
+    // starts at the query's pass-A best, and a partial best prunes extensions as in pass A).
     // per walk: range (start | len << 16), packed best = L << 13 | (8191 - position),
     // query bytes 0..11, x | cap << 13 | tag3 << 22
     uint32_t rs[kQPL];   // result of query r: m (0 = literal, kUnknown)
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    uint32_t *h_x = region + kScanHot + kHotWords * wv;   // hot slot: x | first entry << 13 | ext << 26
+    uint32_t *h_base = h_x + kHotCap;                      // first pair index of the slot
+    uint32_t *h_best = h_base + kHotCap;                   // packed best (bit 31: unknown)
+    uint8_t *h_mk = (uint8_t *)(h_best + kHotCap);         // owner marks of a 64-pair chunk
 #pragma unroll
     for (uint32_t g = 0; g < kQPL; g += kIlp) {
         uint32_t rng[kIlp], best[kIlp], xpk[kIlp], qa[kIlp], qb[kIlp], qc[kIlp];   // rng ~0 = unknown
@@ -998,7 +1023,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     qc[u] = lds_ld4(sdw, x + 8);
                     const uint32_t h = key_mix(qa[u] & 0xFFFFFFu);
                     const uint32_t bk = h >> (24 - kHashBits);
-                    const uint32_t sn = g == 0 ? snap[u] : 0xFFFF0000u | ((slo[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+                    const uint32_t sn = snap[g + u];
                     const uint32_t b0 = h16[bk], b1 = h16[bk + 1];
                     const uint32_t lo = b0 + (sn & 0xFFFFu);
                     const uint32_t n = ((sn >> 16) == 0xFFFFu ? b1 : min(b1, b0 + (sn >> 16))) - lo;
@@ -1008,7 +1033,18 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                 }
             }
         }
-        for (uint32_t j = 0; j < nmax; j++) {
+        // K: binary search for the smallest count with at most kHotCap longer ranges
+        auto nrange = [&](uint32_t u) -> uint32_t { return rng[u] == 0xFFFFFFFFu ? 0u : rng[u] >> 16; };
+        uint32_t klo = 0, khi = wave_max_dpp(nmax);
+        while (klo < khi) {
+            const uint32_t mid = (klo + khi) >> 1;
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < kIlp; u++) c += (uint32_t)__popcll(__ballot(nrange(u) > mid));
+            if (c <= kHotCap) khi = mid; else klo = mid + 1;
+        }
+        const uint32_t K = (dbg & (1u << 20)) ? wave_max_dpp(nmax) : (dbg & (1u << 21)) ? 0u : klo;   // (A/B: all pass A / all pass B)
+        for (uint32_t j = 0; j < K; j++) {
 #pragma unroll
             for (uint32_t u = 0; u < kIlp; u++) {
                 if (j >= (rng[u] >> 16) || rng[u] == 0xFFFFFFFFu) continue;
@@ -1053,6 +1089,88 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                 best[u] = max(best[u], (Lc << 13) | (8191u - xe));
             }
         }
+        // pass B: the hot queries' entries from K on, flattened over the wave
+        bool hot[kIlp];
+        uint32_t slot[kIlp], hbase[kIlp], T = 0, nh = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kIlp; u++) {
+            hot[u] = rng[u] != 0xFFFFFFFFu && (rng[u] >> 16) > K;
+            const uint64_t bal = __ballot(hot[u]);
+            slot[u] = nh + lanes_below(bal);
+            nh += (uint32_t)__popcll(bal);
+            const uint32_t m = hot[u] ? (rng[u] >> 16) - K : 0u;
+            const uint32_t inc = wave_incl_scan(m);
+            hbase[u] = T + inc - m;
+            T += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            if (hot[u]) {
+                h_x[slot[u]] = (xpk[u] & 0x1FFFu) | (((rng[u] & 0xFFFFu) + K) << 13);
+                h_base[slot[u]] = hbase[u];
+                h_best[slot[u]] = best[u];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t c0 = 0; c0 < T; c0 += 64) {
+            if (lane < 16) ((uint32_t *)h_mk)[lane] = 0u;
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (uint32_t u = 0; u < kIlp; u++)
+                if (hot[u] && hbase[u] < c0 + 64 && hbase[u] + (rng[u] >> 16) - K > c0)
+                    h_mk[hbase[u] > c0 ? hbase[u] - c0 : 0] = (uint8_t)(slot[u] + 1);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t hs = wave_incl_max_dpp(h_mk[lane]) - 1u;
+            const uint32_t k = c0 + lane;
+            if (k >= T) continue;
+            const uint32_t hx = h_x[hs];
+            const uint32_t x = hx & 0x1FFFu;
+            const uint32_t nd = ent[((hx >> 13) & 0x1FFFu) + k - h_base[hs]];
+            const uint32_t xe = nd & 0x1FFFu;
+            const uint32_t xlo = max(w0 + x, kWin) - kWin - w0;
+            if (xe >= x || xe < xlo) continue;
+            const uint32_t wq = x >> 2, sq = x & 3;
+            const uint32_t q_0 = sdw[wq], q_1 = sdw[wq + 1];
+            const uint32_t qa1 = __builtin_amdgcn_alignbyte(q_1, q_0, sq);
+            if (((nd >> 13) & 7u) != (key_mix(qa1 & 0xFFFFFFu) & 7u)) continue;
+            const uint32_t wb = xe >> 2, sb = xe & 3;
+            const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1];
+            const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa1;
+            if (d0 & 0xFFFFFFu) continue;
+            const uint32_t cap = min(kMaxL, blen - (w0 + x)) - 1;
+            uint32_t Lc;
+            if (d0) Lc = 3;
+            else {
+                const uint32_t q_2 = sdw[wq + 2], w_2 = sdw[wb + 2];
+                const uint32_t d1 = __builtin_amdgcn_alignbyte(w_2, w_1, sb) ^ __builtin_amdgcn_alignbyte(q_2, q_1, sq);
+                if (d1) Lc = 4 + (__builtin_ctz(d1) >> 3);
+                else {
+                    const uint32_t q_3 = sdw[wq + 3], w_3 = sdw[wb + 3];
+                    const uint32_t d2 = __builtin_amdgcn_alignbyte(w_3, w_2, sb) ^ __builtin_amdgcn_alignbyte(q_3, q_2, sq);
+                    if (d2) Lc = 8 + (__builtin_ctz(d2) >> 3);
+                    else {
+                        // >= 12 bytes, against the slot's partial best (it only grows)
+                        const uint32_t cur = h_best[hs];
+                        if (cur >> 31) continue;   // already unknown
+                        const uint32_t bL = cur >> 13, bxe = 8191u - (cur & 0x1FFFu);
+                        if (cap <= 12 || (dbg & 2u) ||
+                            (bL >= 12 && xe > bxe && (bL >= cap || lds_ld1(sdw, xe + bL) != lds_ld1(sdw, x + bL))))
+                            Lc = 12;
+                        else {
+                            const uint32_t old = atomicAdd(&h_x[hs], 1u << 26);
+                            if ((old >> 26) >= kExtBudget) { atomicOr(&h_best[hs], 0x80000000u); continue; }
+                            Lc = lds_match_len(sdw, xe, x, 12, cap);
+                        }
+                    }
+                }
+            }
+            atomicMax(&h_best[hs], (min(Lc, cap) << 13) | (8191u - xe));
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t u = 0; u < kIlp; u++)
+            if (hot[u]) {
+                const uint32_t b = h_best[slot[u]];
+                if (b >> 31) rng[u] = 0xFFFFFFFFu;
+                else best[u] = b;
+            }
 #pragma unroll
         for (uint32_t u = 0; u < kIlp; u++) {
             const uint32_t x = xpk[u] & 0x1FFFu;

@@ -4,4 +4,6 @@ set -u
 R=$PWD
 timeout -k 10 300 python tools/shardscale.py --kind rand --seed 4 --out gpurun_out/shardscale_rand.json > gpurun_out/shardscale_rand.log 2>&1 || exit 1
 timeout -k 10 300 python tools/shardscale.py --kind text --seed 3 --out gpurun_out/shardscale_text.json > gpurun_out/shardscale_text.log 2>&1 || exit 1
+timeout -k 10 200 python tools/matchphase.py --kind text --seed 3 --mib 256 > gpurun_out/phase_text.log 2>&1 || exit 1
+timeout -k 10 200 python tools/matchphase.py --kind rand --seed 4 --mib 256 > gpurun_out/phase_rand.log 2>&1 || exit 1
 bash tools/gpu_prof_round.sh

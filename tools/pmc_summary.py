@@ -24,7 +24,7 @@ for d in sorted(glob.glob(os.path.join(base, "pmc_*_[AB]"))):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0].replace("fcx::", "")
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("fcx::", "").split("<")[0]
             if not name.startswith("k_"):
                 continue
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
