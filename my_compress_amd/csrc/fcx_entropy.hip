@@ -389,6 +389,7 @@ __global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void
     const uint32_t i0 = c0 + kSymL * tid, i1 = min(c1, i0 + kSymL);
     uint32_t sym[kSymW];
     const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
+    const uint32_t n_chunk = c1 - c0;
     const uint64_t obyte = blk_off[b] + bi.words_rel[s];
     uint64_t *st = cstat + 2 * ((uint64_t)b * L.cpb_total + r);   // this chunk's words; st[-2k]: k chunks back
     bool all8 = true;
@@ -401,11 +402,65 @@ __global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void
     // all 256 symbols with 8-bit codes (the chars of random data): the code stream is a
     // byte substitution
     const bool byte8 = __syncthreads_and(all8) != 0;
+    if (byte8) {
+        // every symbol of the stream is 8 bits: the chunk starts 8 c0 bits into the stream (no
+        // look-back), and its bytes are a substitution.  Whole words inside the chunk are plain
+        // stores; a word shared with the previous or next chunk gets this chunk's bytes only
+        // (byte stores), so no chunk waits for a neighbour.  The stream's last chunk writes
+        // whole words through the stream's W code words (zeros past the codes, 849-928; the
+        // bytes after them belong to headers that k_headers writes later).
+        const uint32_t T = 8 * n_chunk;
+        const uint64_t g0 = 8 * obyte + 8ull * c0;
+        const uint32_t sh0 = (uint32_t)(g0 & 31);
+        const uint32_t nw = (sh0 + T + 31) >> 5;
+        uint32_t *o32 = (uint32_t *)out + (g0 >> 5);
+        for (uint32_t x = tid; x < nw; x += kEncT) ws[x] = 0u;
+        uint32_t v[kSymW + 1];
+#pragma unroll
+        for (uint32_t q = 0; q < kSymW; q++) {
+            const uint32_t w = sym[q];
+            v[q] = ct[w & 0xFF] | (ct[(w >> 8) & 0xFF] << 8) | (ct[(w >> 16) & 0xFF] << 16) | (ct[w >> 24] << 24);
+            if (4 * q >= n) v[q] = 0;
+            else if (n - 4 * q < 4) v[q] &= (1u << (8 * (n - 4 * q))) - 1u;
+        }
+        // this lane's bytes start at staging byte sh0/8 + kSymL tid: shift into kSymW + 1
+        // words, the first and last two shared with the neighbouring lanes
+        const uint32_t bo = (sh0 >> 3) + kSymL * tid, sb = 8 * (bo & 3), w0 = bo >> 2;
+        v[kSymW] = 0;
+        __syncthreads();
+        if (n) {
+            uint32_t prev = 0;
+#pragma unroll
+            for (uint32_t q = 0; q <= kSymW; q++) {
+                const uint32_t cur = v[q];
+                const uint32_t o = sb ? (cur << sb) | (prev >> (32 - sb)) : cur;
+                prev = cur;
+                if (q == 0 || q >= kSymW - 1) { if (o) atomicOr(&ws[w0 + q], o); }
+                else ws[w0 + q] = o;
+            }
+        }
+        __syncthreads();
+        const uint32_t e = sh0 + T;   // end bit in the staging
+        const uint32_t nst = lastc ? (uint32_t)(((8 * obyte + 32ull * bi.nwords[s] - 1) >> 5) - (g0 >> 5) + 1) : nw;
+        const uint32_t xa = sh0 ? 1u : 0u;                                     // first whole word
+        const uint32_t xz = lastc ? nst : ((e & 31) ? nw - 1 : nw);           // end of whole words
+        for (uint32_t x = xa + tid; x < xz; x += kEncT) o32[x] = x < nw ? ws[x] : 0u;
+        // edge words: bytes [sh0/8, 4) of word 0, bytes [0, (e & 31)/8) of word nw - 1
+        uint8_t *o8 = (uint8_t *)o32;
+        if (tid < 4) {
+            const uint32_t q = tid;
+            // word 0 shared with the previous chunk (or the record's header bytes): bytes from sh0/8
+            // (a one-word chunk that is not the stream's last: only up to its end)
+            if (sh0 && q >= (sh0 >> 3) && (lastc || nw > 1 || 8 * q < e)) o8[q] = (uint8_t)(ws[0] >> (8 * q));
+            // the last word shared with the next chunk: bytes below the end bit
+            if (!lastc && (e & 31) && !(nw == 1 && sh0) && 8 * q < (e & 31))
+                o8[4 * (nw - 1) + q] = (uint8_t)(ws[nw - 1] >> (8 * q));
+        }
+        return;
+    }
     // ---- this chunk's bit count and this lane's bit offset in it
     uint32_t nb = 0;
-    if (byte8) nb = 8 * n;
-    else
-        for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
+    for (uint32_t q = 0; q < n; q++) nb += lt[(sym[q >> 2] >> (8 * (q & 3))) & 0xFF];
     const uint32_t inc = wave_incl_scan(nb);
     if (lane == 63) red[wv] = inc;
     __syncthreads();
@@ -455,38 +510,6 @@ __global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void
                                : (((sh0 + T) & 31) == 0 ? nw : nw - 1);
     uint32_t *o32 = (uint32_t *)out + (g0 >> 5);
     uint32_t w0v = 0;   // (thread 0) the first staged word, kept for the merge
-    if (byte8) {
-        for (uint32_t x = tid; x < nw; x += kEncT) ws[x] = 0u;
-        uint32_t v[kSymW + 1];
-#pragma unroll
-        for (uint32_t q = 0; q < kSymW; q++) {
-            const uint32_t w = sym[q];
-            v[q] = ct[w & 0xFF] | (ct[(w >> 8) & 0xFF] << 8) | (ct[(w >> 16) & 0xFF] << 16) | (ct[w >> 24] << 24);
-            if (4 * q >= n) v[q] = 0;
-            else if (n - 4 * q < 4) v[q] &= (1u << (8 * (n - 4 * q))) - 1u;
-        }
-        // this lane's bytes start at staging byte sh0/8 + kSymL tid: shift into kSymW + 1
-        // words, the first and last two shared with the neighbouring lanes
-        const uint32_t bo = (sh0 >> 3) + kSymL * tid, sb = 8 * (bo & 3), w0 = bo >> 2;
-        v[kSymW] = 0;
-        __syncthreads();
-        if (n) {
-            uint32_t prev = 0;
-#pragma unroll
-            for (uint32_t q = 0; q <= kSymW; q++) {
-                const uint32_t cur = v[q];
-                const uint32_t o = sb ? (cur << sb) | (prev >> (32 - sb)) : cur;
-                prev = cur;
-                if (q == 0 || q >= kSymW - 1) { if (o) atomicOr(&ws[w0 + q], o); }
-                else ws[w0 + q] = o;
-            }
-        }
-        __syncthreads();
-        if (!lastc && tid == 0) publish_tail(st, ws, sh0 + T);
-        for (uint32_t x = (merge ? 1 : 0) + tid; x < nst; x += kEncT) o32[x] = x < nw ? ws[x] : 0u;
-        if (merge && tid == 0) merge_head(st, o32, ws[0], sh0);
-        return;
-    }
     // this lane's codes cover bits [p0, p1) of the staging words; whole words inside
     // that range are this lane's alone (plain LDS stores), the two end words are shared.
     // Windows of kEncWords words: a lane writes the words of its range inside the window.
