@@ -791,6 +791,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     const uint32_t mk1 = last ? binfo[b].nmatch : tile_off[3 * tix + 4];
     const uint32_t cv = tconv[tix];
     const bool uni = (tinfo[8 * tix] & kTileUniform) != 0;   // m = m_uniform, no rows
+    const uint32_t nspec = tinfo[8 * tix + 3];   // match tokens of the speculative chain (its compact list)
     const uint32_t s = t0 + tid * 16;   // this lane's 16 positions: one quarter of a chain word
     uint64_t cwv = 0, mbv = 0;
     if (s < t1) {
@@ -918,10 +919,9 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     }
     const uint32_t rd = bits & mbs & ~post;   // chain positions whose m is in m[]
     const uint32_t rc = bits & mbs & post;    // chain matches in the compact list
-    uint32_t cbase = (uint32_t)__builtin_popcount(rc), ncomp;
-    block_scan1t(cbase, ncomp, sh + 12);       // (also publishes lin)
 
-    // ---- round 2: m rows and the compact list ----
+    // ---- round 2: m rows and the compact list, issued before the scan (they need only round-1
+    // values: the list from the conv point holds at most the speculative matches not dropped) ----
     const uint32_t *mt = m + bstart + s;
     uint32_t mm[16];
     if (uni) {
@@ -937,12 +937,15 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
 #pragma unroll
         for (uint32_t q = 0; q < 16; q++) mm[q] = ((rd >> q) & 1u) ? mt[q] : 0u;
     }
+    uint32_t cbase = (uint32_t)__builtin_popcount(rc), ncomp;
     {   // the list starts at the tile's first speculative position: skip the matches the
         // final chain dropped before the conv point
         const uint32_t *mct = mtok + (uint64_t)tix * kTileMatches + (cv >> 16);
+        const uint32_t nl = crel != kConvAll && nspec > (cv >> 16) ? nspec - (cv >> 16) : 0u;
         uint32_t cl[kTileMatches / 256];
 #pragma unroll
-        for (uint32_t u = 0; u < kTileMatches / 256; u++) cl[u] = tid + 256 * u < ncomp ? mct[tid + 256 * u] : 0u;
+        for (uint32_t u = 0; u < kTileMatches / 256; u++) cl[u] = tid + 256 * u < nl ? mct[tid + 256 * u] : 0u;
+        block_scan1t(cbase, ncomp, sh + 12);       // (also publishes lin)
 #pragma unroll
         for (uint32_t u = 0; u < kTileMatches / 256; u++) lmt[tid + 256 * u] = cl[u];
     }
