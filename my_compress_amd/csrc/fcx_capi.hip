@@ -19,7 +19,8 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev);
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev,
+                  uint32_t emit_dbg = 0);
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
                     const uint16_t *thist, const uint32_t *bhist, const uint32_t *tile_off, uint32_t *ctab,
                     uint8_t *ltab, uint8_t *hhdr, uint64_t *cstat, uint64_t *blk_off, uint64_t *total, uint8_t *out,
@@ -115,6 +116,7 @@ struct fcx_ctx {
     // profiling
     bool profiling = false;
     uint32_t match_mode = 0;   // k_match tile-mode bits (fcx_ctx_set_match_mode)
+    uint32_t emit_dbg = 0;     // k_emit development exits (fcx_debug_emit_bits; output invalid)
     hipEvent_t ev[kMaxGroups][kNumStages + 1] = {};
     uint32_t ngroups_timed = 0;
     bool have_times = false;
@@ -361,7 +363,12 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         launch_parse(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
                      c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 8 * t0,
                      c->tile_off + 3 * t0, c->tconv + t0, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3],
-                     c->thist + t0 * 256, c->bhist + b0 * kStreams * 256, sg, ev ? ev + 3 : nullptr);
+                     c->thist + t0 * 256, c->bhist + b0 * kStreams * 256, sg, ev ? ev + 3 : nullptr, c->emit_dbg);
+        if (c->emit_dbg) {   // (development: k_emit's timing exits leave invalid streams; stop here)
+            if (ev)
+                for (int q = 5; q <= kNumStages; q++) HIP_TRY(hipEventRecord(ev[q], sg));
+            continue;
+        }
         launch_entropy(Lg, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3], c->thist + t0 * 256,
                        c->bhist + b0 * kStreams * 256, c->tile_off + 3 * t0, c->ctab + b0 * kStreams * 256,
                        c->ltab + b0 * kStreams * 256, c->hhdr + b0 * kStreams * kHuffHdrStride,
@@ -412,6 +419,14 @@ int fcx_ctx_stats(fcx_ctx *c, uint64_t *tokens, uint64_t *matches, uint64_t *laz
         for (auto &x : bi) tl += (x.len + kTile - 1) / kTile;
         *tiles = tl;
     }
+    return FCX_OK;
+}
+
+// development only (not in fcx.h): k_emit's timing exits for the following compress calls (their
+// output is invalid while bits are set; 0 restores the product kernel)
+int fcx_debug_emit_bits(fcx_ctx *c, uint32_t bits) {
+    if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
+    c->emit_dbg = bits;
     return FCX_OK;
 }
 

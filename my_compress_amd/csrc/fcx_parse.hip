@@ -760,13 +760,17 @@ constexpr uint32_t kInW = (kTile + kLookAhead) / 4 + 2;   // tile input + look-a
 // offsets, conv record, chain and mbits words, the tile's input + look-ahead into LDS);
 // after one block scan, the second and last round of loads (m rows, the compact match
 // list into LDS); everything after that is LDS work and stores.
+// kDev = true carries development exits (timing of the paths, output discarded: fcx_debug_emit_bits);
+// the product launches k_emit<false>
+template <bool kDev>
 __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, Layout L, const uint32_t *__restrict__ m,
                                               const uint64_t *__restrict__ mbits, const uint64_t *__restrict__ chain, const uint32_t *__restrict__ tile_off,
                                               const BlockInfo *__restrict__ binfo, const uint32_t *__restrict__ mtok,
                                               const uint32_t *__restrict__ tconv, const uint32_t *__restrict__ tinfo,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb,
-                                              uint16_t *__restrict__ thist, uint32_t *__restrict__ bhist) {
+                                              uint16_t *__restrict__ thist, uint32_t *__restrict__ bhist, uint32_t dbg_in) {
+    const uint32_t dbg = kDev ? dbg_in : 0u;
     __shared__ uint32_t sh[16];
     __shared__ uint32_t hh[kStreams][256];   // this tile's symbol counts per stream
     __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW], lc[kCharW];
@@ -887,6 +891,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     if (tid < kInW - kTile / 4) lin[kTile / 4 + tid] = la;
 
     if (tk1 - tok0 == t1 - t0 && mk1 == mi0) {   // no match token in the tile (uniform)
+        if (dbg & 1u) { if (s < t1 && (in4[0] ^ (uint32_t)cwv) == 0x12345u) trow[tid] = 1; return; }   // (timing)
         __syncthreads();
         emit_literal_tile(lin, t1 - t0, tok0, s_chars + (uint64_t)b * L.sstride[1],
                           (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]));
@@ -901,6 +906,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         return;
     }
 
+    if (dbg & 2u) { if (s < t1 && (in4[0] ^ (uint32_t)cwv ^ (uint32_t)mbv ^ cv) == 0x12345u) trow[tid] = 1; return; }
     uint32_t bits = 0, mbs = 0;
     if (s < t1) {
         bits = (uint32_t)(cwv >> (16 * (tid & 3))) & 0xFFFFu;
@@ -954,6 +960,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     for (uint32_t w = tid; w < kGW; w += 256) lg[w] = 0;
     for (uint32_t w = tid; w < kCharW; w += 256) lc[w] = 0;
     __syncthreads();
+    if (dbg & 4u) { if (lmt[tid] == 0x12345u && mm[0] == 7u) trow[tid] = 1; return; }   // (timing: + round 2)
 
     uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0};
 #pragma unroll
@@ -1005,7 +1012,6 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
             } else {
                 pacc |= (uint64_t)m_dist(mm[q]) << (kPBits * np_lane);
                 np_lane++;
-                // q one-bits, a zero bit, then r (2 bits, LSB first)
                 const uint32_t qq = Lm >> 2, r = Lm & 3;
                 uint32_t pos = goff, left = qq;
                 while (left) {
@@ -1025,6 +1031,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     or_bits64(lf, fw0, tokA, fl, nt_lane);
     or_bits64(lp, pw0, (uint64_t)kPBits * miA, pacc, kPBits * nm_lane);
     __syncthreads();
+    if (dbg & 8u) { if (lf[tid & 63] == 0x12345u) trow[tid] = 1; return; }   // (timing: + token loop)
 
     // chars: aligned dwords inside the tile's range, bytes at its two edges
     uint8_t *chars = s_chars + (uint64_t)b * L.sstride[1];
@@ -1055,14 +1062,19 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev) {
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev,
+                  uint32_t emit_dbg) {
     const uint32_t ntiles = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_resolve, dim3(ntiles), dim3(64), 0, st, L, m, mbits, chain, chain_pfx, tinfo, fp);
     hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, mtok,
                        tile_off, tconv, binfo, s_flags, s_p, s_golomb, bhist);
     if (ev) (void)hipEventRecord(ev[0], st);
-    hipLaunchKernelGGL(k_emit, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok, tconv,
-                       tinfo, s_flags, s_chars, s_p, s_golomb, thist, bhist);
+    if (emit_dbg == 0)
+        hipLaunchKernelGGL(k_emit<false>, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok,
+                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, bhist, 0u);
+    else
+        hipLaunchKernelGGL(k_emit<true>, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok,
+                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, bhist, emit_dbg);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 
