@@ -88,7 +88,7 @@ __device__ inline const uint8_t *stream_base(const Layout &L, uint32_t s, uint32
 }
 
 // ---------------------------------------------------------------------------
-constexpr uint32_t kTreeT = 128;   // k_tree workgroup: two waves (more trees per CU: the merge is serial)
+constexpr uint32_t kTreeT = 256;   // k_tree workgroup: four waves (the chars rows are summed by all of them; the merge is serial)
 constexpr uint32_t kTreeW = kTreeT / 64;
 
 __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__restrict__ thist,
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
     if (s == 1) {   // chars: wave wv sums the tile rows t = wv mod kTreeW (lane: symbols 4 lane .. 4 lane + 3)
         const uint2 *rows = (const uint2 *)(thist + (uint64_t)b * L.tpb * 256);
         uint32_t acc[4] = {0, 0, 0, 0};
-#pragma unroll 8
+#pragma unroll 16
         for (uint32_t t = wv; t < ntl; t += kTreeW) {
             const uint2 v = rows[(uint64_t)t * 64 + lane];
             acc[0] += v.x & 0xFFFFu; acc[1] += v.x >> 16; acc[2] += v.y & 0xFFFFu; acc[3] += v.y >> 16;
