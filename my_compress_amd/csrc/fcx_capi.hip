@@ -164,7 +164,7 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     if ((r = dalloc(&c->tile_off, 12 * nt, "tile_off"))) return r;
     if ((r = dalloc(&c->mtok, 4ull * kTileMatches * nt, "mtok"))) return r;
     if ((r = dalloc(&c->tconv, 4 * nt, "tconv"))) return r;
-    if ((r = dalloc(&c->fp, 64 * nt, "fp"))) return r;
+    if ((r = dalloc(&c->fp, 96 * nt, "fp"))) return r;   // 12 u64 per tile (k_resolve record)
     if ((r = dalloc(&c->binfo, sizeof(BlockInfo) * nb, "binfo"))) return r;
     for (uint32_t s = 0; s < kStreams; s++)
         if ((r = dalloc(&c->s[s], (uint64_t)L.sstride[s] * nb + 64, "stream"))) return r;
@@ -361,7 +361,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                      c->match_mode);
         if (ev) HIP_TRY(hipEventRecord(ev[2], sg));
         launch_parse(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
-                     c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 8 * t0,
+                     c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 12 * t0,
                      c->tile_off + 3 * t0, c->tconv + t0, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3],
                      c->thist + t0 * 256, c->bhist + b0 * kStreams * 256, sg, ev ? ev + 3 : nullptr, c->emit_dbg);
         if (c->emit_dbg) {   // (development: k_emit's timing exits leave invalid streams; stop here)

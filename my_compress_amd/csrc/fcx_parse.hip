@@ -186,9 +186,13 @@ __device__ Cnt3 spec_prefix_c(const uint64_t *pfx, const uint32_t *mtt, const ui
 //       conv = rel | dropped speculative matches << 16 where the walk met the
 //       speculative chain, kConvAll if it walked to the tile end)
 //   [3] exit (first chain position >= t1)
-//   [4..7] the rewritten chain words 0..3 (positions t0 .. t0+255)
-// ok = 0 when the walk needs > 256 positions, meets an unknown position, or a
-// neighbour is lazy: the stitch then walks the tile itself.
+//   [4..11] the rewritten chain words 0..nmod-1 (positions t0 .. t0 + 64 nmod - 1)
+// The walk reaches kResolveSpan positions, kRmSpan on run-mode tiles (their m rows are exact that
+// far: long tokens take longer to meet the speculative chain).  ok = 0 when the walk needs more,
+// meets an unknown position, or a neighbour is lazy: the stitch then walks the tile itself.
+constexpr uint32_t kFpStride = 12;               // u64 per tile record
+constexpr uint32_t kResW = kRmSpan / 64;         // chain words a walk may rewrite
+static_assert(kFpStride >= 4 + kResW && kRmSpan >= kResolveSpan, "resolve record");
 
 __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__restrict__ m,
                                                 const uint64_t *__restrict__ mbits,
@@ -202,17 +206,18 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     const uint32_t t0 = k * kTile;
     if (t0 >= blen) return;
     const uint32_t t1 = min(blen, t0 + kTile);
-    uint64_t *out = fp + 8ull * tix;
+    uint64_t *out = fp + (uint64_t)kFpStride * tix;
     const uint32_t *ti = tinfo + 8ull * tix;
     bool ok = (ti[0] & kTileLazy) == 0;
     const bool uni = (ti[0] & kTileUniform) != 0;   // m = m_uniform, no rows
+    const uint32_t span = (ti[0] & kTileSpan2) ? kRmSpan : kResolveSpan;   // m rows exact below it
     uint32_t ea = t0;
     if (ok && k > 0) {
         const uint32_t *tp = tinfo + 8ull * (tix - 1);
         ok = (tp[0] & kTileLazy) == 0;
         ea = tp[1];
     }
-    ok = ok && ea < t1 && ea - t0 < kResolveSpan;
+    ok = ok && ea < t1 && ea - t0 < span;
     if (!ok) {
         if (lane == 0) out[0] = 0;
         return;
@@ -221,42 +226,43 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     const uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
     const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
     const uint32_t *mt = m + bstart + t0;
-    const uint32_t nw = min(4u, (t1 - t0 + 63) / 64);
-    // prefetch: chain + mbits words 0..3 (lanes 0..3), m of positions t0..t0+255 (4 per lane)
+    const uint32_t nw = min(span / 64, (t1 - t0 + 63) / 64);
+    // prefetch: chain + mbits words below the span (lanes 0..nw-1), m of those positions
     uint64_t wv = 0, mv = 0;
     if (lane < nw) { wv = cw[lane]; mv = mb[lane]; }
-    uint32_t mreg[4];
+    uint32_t mreg[kResW];
 #pragma unroll
-    for (uint32_t q = 0; q < 4; q++) {
+    for (uint32_t q = 0; q < kResW; q++) {
         const uint32_t x = 64 * q + lane;
         const uint64_t mbq = __shfl(mv, q, 64);
-        mreg[q] = (x < t1 - t0 && ((mbq >> lane) & 1ull)) ? (uni ? m_uniform(t0 + x, blen) : mt[x]) : 0u;
+        mreg[q] = (q < nw && x < t1 - t0 && ((mbq >> lane) & 1ull)) ? (uni ? m_uniform(t0 + x, blen) : mt[x]) : 0u;
     }
-    uint64_t orig[4], mbw[4], nwb[4];
-#pragma unroll
-    for (uint32_t q = 0; q < 4; q++) { orig[q] = __shfl(wv, q, 64); mbw[q] = __shfl(mv, q, 64); nwb[q] = 0; }
+    // chain / mbits words stay distributed (lane q holds word q); the walk reads word q of the
+    // wave-uniform position by readlane, and lane q keeps the walked bits of word q
+    auto word_at = [](uint64_t v, uint32_t q) -> uint64_t {
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)q) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)q) << 32);
+    };
+    uint64_t nwb = 0;
     // walk from the assumed entry until it meets the speculative chain (uniform over the wave)
     Cnt3 walked{0, 0, 0};
     uint32_t rel = rel0, exitv = 0;
     bool conv = false;
     for (;;) {
         if (rel >= t1 - t0) { exitv = t0 + rel; break; }
-        if (rel >= kResolveSpan) { ok = false; break; }
-        const uint32_t q = rel >> 6, r = rel & 63;
-        uint64_t o = orig[0], mbq = mbw[0];
-#pragma unroll
-        for (uint32_t u = 1; u < 4; u++) if (q == u) { o = orig[u]; mbq = mbw[u]; }
+        if (rel >= span) { ok = false; break; }
+        const uint32_t q = fcx::uni(rel >> 6), r = rel & 63;
+        const uint64_t o = word_at(wv, q), mbq = word_at(mv, q);
         if ((o >> r) & 1ull) { conv = true; break; }
         uint32_t mm = 0;
         if ((mbq >> r) & 1ull) {
             uint32_t v = mreg[0];
 #pragma unroll
-            for (uint32_t u = 1; u < 4; u++) if (q == u) v = mreg[u];
+            for (uint32_t u = 1; u < kResW; u++) if (q == u) v = mreg[u];
             mm = __shfl(v, r, 64);
         }
         if (mm == kUnknown) { ok = false; break; }
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) if (q == u) nwb[u] |= 1ull << r;
+        if (lane == q) nwb |= 1ull << r;
         walked.add(m_len(mm));
         rel += m_len(mm) + 1;
     }
@@ -268,8 +274,8 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     uint32_t keep_from = rel;   // speculative bits at positions >= keep_from stay
     uint32_t convrec = kConvAll;
     if (conv) {
-        const Cnt3 drop = rel ? spec_prefix(chain_pfx + (uint64_t)tix * (kTile / 64), mt, mb, orig[rel >> 6], rel, uni,
-                                            t0, blen)
+        const Cnt3 drop = rel ? spec_prefix(chain_pfx + (uint64_t)tix * (kTile / 64), mt, mb, word_at(wv, fcx::uni(rel >> 6)),
+                                            rel, uni, t0, blen)
                               : Cnt3{0, 0, 0};
         fin.tok += ti[2] - drop.tok;
         fin.mat += ti[3] - drop.mat;
@@ -280,17 +286,16 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
         keep_from = t1 - t0;   // the walk covered the rest of the tile
     }
     // rewritten words: walked bits below keep_from, speculative bits from keep_from on
-    const uint32_t nmod = min(nw, (min(keep_from, kResolveSpan) + 63) / 64);
+    const uint32_t nmod = min(nw, (min(keep_from, span) + 63) / 64);
+    if (lane < nmod) {
+        const uint32_t lo = 64 * lane;
+        uint64_t keepmask;
+        if (keep_from <= lo) keepmask = ~0ull;
+        else if (keep_from >= lo + 64) keepmask = 0;
+        else keepmask = ~0ull << (keep_from - lo);
+        out[4 + lane] = (wv & keepmask) | nwb;
+    }
     if (lane == 0) {
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-            const uint32_t lo = 64 * u;
-            uint64_t keepmask;
-            if (keep_from <= lo) keepmask = ~0ull;
-            else if (keep_from >= lo + 64) keepmask = 0;
-            else keepmask = ~0ull << (keep_from - lo);
-            out[4 + u] = (orig[u] & keepmask) | nwb[u];
-        }
         out[0] = 1ull | ((uint64_t)rel0 << 1) | ((uint64_t)nmod << 16);
         out[1] = (uint64_t)fin.tok | ((uint64_t)fin.mat << 32);
         out[2] = fin.gb | ((uint64_t)convrec << 32);
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
     __shared__ uint32_t mL[kTile];
     __shared__ uint32_t sti[64][6];          // per tile of the batch: flags, exit, totals, k_resolve verdict
     __shared__ uint32_t sfp[64][5];          // k_resolve: final counts, exit, conv record
-    __shared__ uint64_t sfw[64][4];          // k_resolve: rewritten chain words
+    __shared__ uint64_t sfw[64][kResW];      // k_resolve: rewritten chain words
     __shared__ uint64_t bmL[kTile / 64];
     __shared__ uint64_t mbL[kTile / 64];
     __shared__ uint32_t dw[kLazyWindow / 4 + 4];
@@ -381,7 +386,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
             const uint32_t kk = k + lane;
             if (kk < ntiles) {
                 const uint32_t *tq = tinfo + 8ull * (b * L.tpb + kk);
-                const uint64_t *fq = fp + 8ull * (b * L.tpb + kk);
+                const uint64_t *fq = fp + (uint64_t)kFpStride * (b * L.tpb + kk);
                 sti[lane][0] = tq[0]; sti[lane][1] = tq[1]; sti[lane][2] = tq[2];
                 sti[lane][3] = tq[3]; sti[lane][4] = tq[4];
                 const uint64_t f0 = fq[0];
@@ -391,7 +396,8 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                     sfp[lane][0] = (uint32_t)f1; sfp[lane][1] = (uint32_t)(f1 >> 32);
                     const uint64_t f2 = fq[2];
                     sfp[lane][2] = (uint32_t)f2; sfp[lane][3] = (uint32_t)fq[3]; sfp[lane][4] = (uint32_t)(f2 >> 32);
-                    for (uint32_t u = 0; u < 4; u++) sfw[lane][u] = fq[4 + u];
+                    const uint32_t nmod = (uint32_t)(f0 >> 16) & 0xFFu;
+                    for (uint32_t u = 0; u < nmod; u++) sfw[lane][u] = fq[4 + u];
                 }
             }
             __syncthreads();
