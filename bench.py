@@ -49,10 +49,11 @@ HL_DIGEST = {  # reference output digests of whole files (SURVEY.md §8(c) / B.4
     ("rand", 2, 64 << 20, 1 << 16): ("3b6853f2cf570b7a35c469efff62c15e0290b04ede45f6b47a97afc82c1878a5", 68819158),
 }
 SEEDS = {"rand": 4, "text": 3, "runs": 5, "zeros": 0, "dna": 6}
-# extra legs after the main one: name -> (kind, block bytes); BASELINE configs 3 and 5, plus
-# "dna" (rand()%4 bytes: dense 3-byte buckets, the lazy-evaluation path)
-LEGS = {"text": ("text", 1 << 20), "c3": ("text", 1 << 18), "zeros": ("zeros", 1 << 20),
-        "runs": ("runs", 1 << 20), "dna": ("dna", 1 << 20)}
+# extra legs after the main one: name -> (kind, block bytes[, seed, MiB]); BASELINE configs 2
+# (64 MiB of seed-2 random bytes at 64 KiB blocks), 3 and 5, plus "dna" (rand()%4 bytes: dense
+# 3-byte buckets, the lazy-evaluation path)
+LEGS = {"c2": ("rand", 1 << 16, 2, 64), "text": ("text", 1 << 20), "c3": ("text", 1 << 18),
+        "zeros": ("zeros", 1 << 20), "runs": ("runs", 1 << 20), "dna": ("dna", 1 << 20)}
 
 
 def log(*a):
@@ -111,16 +112,17 @@ def timed(fn, steps, dist, dev):
     return max_over_ranks(time.perf_counter() - t0, dist, dev)
 
 
-def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, scaling="strong", main_leg=False):
-    """one leg.  strong: the global input of args.global_mib MiB split over the ranks;
-    weak: args.mib MiB per rank (rand: rank r = bytes [r*shard, (r+1)*shard) of one stream)."""
+def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, scaling="strong", main_leg=False,
+            global_mib=None):
+    """one leg.  strong: the global input of global_mib (default args.global_mib) MiB split over
+    the ranks; weak: args.mib MiB per rank (rand: rank r = bytes [r*shard, (r+1)*shard) of one stream)."""
     import torch
 
     import my_compress_amd as mc
     from my_compress_amd import dist as fdist
 
     if scaling == "strong":
-        n_global = args.global_mib << 20
+        n_global = (global_mib or args.global_mib) << 20
         lo, hi = fdist.byte_range(n_global, block, rank, world)
     else:
         per = args.mib << 20
@@ -507,7 +509,7 @@ def main():
     ap.add_argument("--mib", type=int, default=1024, help="MiB per rank for weak scaling (the weak leg)")
     ap.add_argument("--block", type=int, default=1 << 20)
     ap.add_argument("--no-text", action="store_true", help="skip every extra leg")
-    ap.add_argument("--legs", default="text,c3,zeros,runs,dna",
+    ap.add_argument("--legs", default="c2,text,c3,zeros,runs,dna",
                     help="extra legs after the main one (comma list of " + ",".join(LEGS) + ")")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling (config 4) leg at N > 1")
     ap.add_argument("--concat", default="gather", choices=["gather", "allgather", "none"])
@@ -557,10 +559,11 @@ def main():
                        scaling=args.scaling, main_leg=True)
     legs = {}
     for name in ([] if args.no_text else [x for x in args.legs.split(",") if x]):
-        kind, block = LEGS[name]
-        if kind == args.kind and block == args.block:
+        kind, block = LEGS[name][:2]
+        seed, mib = (LEGS[name][2], LEGS[name][3]) if len(LEGS[name]) > 2 else (SEEDS[kind], None)
+        if kind == args.kind and block == args.block and seed == SEEDS[kind] and mib is None:
             continue
-        legs[name] = run_leg(kind, SEEDS[kind], block, args, rank, world, dev, dist, True)
+        legs[name] = run_leg(kind, seed, block, args, rank, world, dev, dist, True, global_mib=mib)
     weak = None
     if dist and not args.no_weak and args.scaling == "strong":
         weak = run_leg("rand", 4, 1 << 20, args, rank, world, dev, dist, False, scaling="weak")
@@ -594,7 +597,8 @@ def main():
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: glibc rand()%256 seed 4 (SURVEY.md §8(d)); the 1 GiB input is SURVEY's HL-rand "
                     "(= the first GiB of BASELINE config 4); extra legs: text = enwik-style generator seed 3 at "
-                    "1 MiB (HL-text) and 256 KiB blocks (C3), zeros and runs seed 5 (config 5), dna = "
+                    "1 MiB (HL-text) and 256 KiB blocks (C3), c2 = rand seed 2, 64 MiB at 64 KiB blocks (config 2), zeros "
+                    "and runs seed 5 (config 5), dna = "
                     "'ACGT'[rand()%4] seed 6 (lazy-path stress)",
             "config": {"workload": f"{args.kind} {main_res['global_bytes'] >> 20} MiB, {args.block // 1024} KiB "
                                    f"blocks, {shard_note}; step = compress + concatenation of the segments "
@@ -618,7 +622,7 @@ def main():
         if world == 1 and not args.no_lz78 and not args.no_text:
             line["lz78"] = lz78_leg(dev)
         keep = ["value", "ms_per_step", "compress_only", "concat_ms_per_step", "ratio", "block_bytes", "stages_ms",
-                "lazy_evals", "lazy_tiles", "decode", "bit_exact_vs_reference"]
+                "lazy_evals", "lazy_tiles", "decode", "bit_exact_vs_reference", "global_bytes"]
         for name, lr in legs.items():
             line[name] = {k: lr[k] for k in keep if k in lr}
         if weak is not None:
