@@ -25,7 +25,8 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
                     const uint16_t *thist, const uint32_t *bhist, const uint32_t *tile_off, uint32_t *ctab,
                     uint8_t *ltab, uint8_t *hhdr, uint64_t *cstat, uint64_t *blk_off, uint64_t *total, uint8_t *out,
                     uint64_t cap, uint32_t *err, hipStream_t st, hipEvent_t *ev, hipEvent_t wait_scan,
-                    hipEvent_t rec_scan);
+                    hipEvent_t rec_scan,
+                    uint32_t tree_dbg = 0);
 }  // namespace fcx
 
 using namespace fcx;
@@ -364,7 +365,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                      c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 12 * t0,
                      c->tile_off + 3 * t0, c->tconv + t0, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3],
                      c->thist + t0 * 256, c->bhist + b0 * kStreams * 256, sg, ev ? ev + 3 : nullptr, c->emit_dbg);
-        if (c->emit_dbg) {   // (development: k_emit's timing exits leave invalid streams; stop here)
+        if (c->emit_dbg & 0xFFFFu) {   // (development: k_emit's timing exits leave invalid streams; stop here)
             if (ev)
                 for (int q = 5; q <= kNumStages; q++) HIP_TRY(hipEventRecord(ev[q], sg));
             continue;
@@ -373,7 +374,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                        c->bhist + b0 * kStreams * 256, c->tile_off + 3 * t0, c->ctab + b0 * kStreams * 256,
                        c->ltab + b0 * kStreams * 256, c->hhdr + b0 * kStreams * kHuffHdrStride,
                        c->cstat + 2 * b0 * L.cpb_total, c->blk_off + b0, total, d_out, cap, err, sg, ev ? ev + 5 : nullptr,
-                       G > 1 && g > 0 ? c->gsync[3 + g - 1] : nullptr, G > 1 ? c->gsync[3 + g] : nullptr);
+                       G > 1 && g > 0 ? c->gsync[3 + g - 1] : nullptr, G > 1 ? c->gsync[3 + g] : nullptr, c->emit_dbg >> 16);
     }
     if (G > 1) {
         for (uint32_t q = 0; q < 2; q++) {
@@ -422,8 +423,8 @@ int fcx_ctx_stats(fcx_ctx *c, uint64_t *tokens, uint64_t *matches, uint64_t *laz
     return FCX_OK;
 }
 
-// development only (not in fcx.h): k_emit's timing exits for the following compress calls (their
-// output is invalid while bits are set; 0 restores the product kernel)
+// development only (not in fcx.h): k_emit's (bits 0..15) and k_tree's (bits 16..) timing exits for the
+// following compress calls (their output is invalid while bits are set; 0 restores the product kernels)
 int fcx_debug_emit_bits(fcx_ctx *c, uint32_t bits) {
     if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
     c->emit_dbg = bits;

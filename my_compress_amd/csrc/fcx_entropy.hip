@@ -91,13 +91,18 @@ __device__ inline const uint8_t *stream_base(const Layout &L, uint32_t s, uint32
 constexpr uint32_t kTreeT = 256;   // k_tree workgroup: four waves (the chars rows are summed by all of them; the merge is serial)
 constexpr uint32_t kTreeW = kTreeT / 64;
 
+// kDev = true carries development timing exits (fcx_debug_emit_bits bits 16..19; the compress stops
+// after this kernel while they are set); the product launches k_tree<false>
+template <bool kDev>
 __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__restrict__ thist,
                                                  const uint32_t *__restrict__ bhist,
                                                  const uint32_t *__restrict__ tile_off, const uint8_t *__restrict__ s0,
                                                  const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
                                                  BlockInfo *__restrict__ binfo, uint32_t *__restrict__ ctab,
                                                  uint8_t *__restrict__ ltab, uint8_t *__restrict__ hhdr,
-                                                 uint64_t *__restrict__ cstat, uint32_t *__restrict__ err) {
+                                                 uint64_t *__restrict__ cstat, uint32_t *__restrict__ err,
+                                                 uint32_t dbg_in) {
+    const uint32_t dbg = kDev ? dbg_in : 0u;
     __shared__ __attribute__((aligned(16))) uint32_t w[256];
     __shared__ uint32_t sw[257], ss[257], ln[256];   // (the merge reads the leaf queue two deep)
     __shared__ uint32_t iw[256], il[256], ir[256], par[512];
@@ -157,6 +162,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
         }
         __syncthreads();
     }
+    if (dbg & 1u) { if (w[tid] == 0x12345u) err[1] = 1; return; }   // (timing: weights only)
     uint32_t nz = 0;
 #pragma unroll
     for (uint32_t u = 0; u < 256 / kTreeT; u++) nz += w[tid + kTreeT * u] != 0 ? 1u : 0u;
@@ -180,6 +186,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
         }
     }
     __syncthreads();
+    if (dbg & 2u) { if (sw[tid] == 0x12345u) err[1] = 1; return; }   // (timing: + rank sort)
     const uint32_t nint = real >= 2 ? real - 1 : 0;
     if (tid == 0 && nint) {
         // two-queue merge == the reference's sorted-list re-insertion (570-611).  Each step
@@ -206,6 +213,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
         }
     }
     __syncthreads();
+    if (dbg & 4u) { if (iw[tid] == 0x12345u) err[1] = 1; return; }   // (timing: + merge)
     const uint32_t root = 256 + nint - 1;
     uint32_t bits = 0;   // this thread's symbols' share of the stream's code bits
 #pragma unroll
@@ -227,6 +235,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
         ln[sym] = len;
         bits += w[sym] * len;
     }
+    if (dbg & 8u) { if (bits == 0x12345u) err[1] = 1; return; }   // (timing: + codes)
     const uint32_t wsum = wave_sum_u32(bits);
     if (lane == 0) s_red[wv] = wsum;
     __syncthreads();
@@ -593,11 +602,18 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
                     const uint16_t *thist, const uint32_t *bhist, const uint32_t *tile_off, uint32_t *ctab,
                     uint8_t *ltab, uint8_t *hhdr, uint64_t *cstat, uint64_t *blk_off, uint64_t *total, uint8_t *out,
                     uint64_t cap, uint32_t *err, hipStream_t st, hipEvent_t *ev, hipEvent_t wait_scan,
-                    hipEvent_t rec_scan) {
+                    hipEvent_t rec_scan, uint32_t tree_dbg) {
     const uint32_t nchunks = L.nblocks * L.cpb_total;
     if (ev) (void)hipEventRecord(ev[0], st);   // (the histograms are k_emit's: no stage of their own)
-    hipLaunchKernelGGL(k_tree, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, bhist, tile_off, s0, s2, s3,
-                       binfo, ctab, ltab, hhdr, cstat, err);
+    if (tree_dbg) {   // (development: k_tree's timing exits; nothing after it runs)
+        hipLaunchKernelGGL(k_tree<true>, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, bhist, tile_off, s0,
+                           s2, s3, binfo, ctab, ltab, hhdr, cstat, err, tree_dbg);
+        if (ev)
+            for (int q = 1; q <= 6; q++) (void)hipEventRecord(ev[q], st);
+        return;
+    }
+    hipLaunchKernelGGL(k_tree<false>, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, bhist, tile_off, s0, s2,
+                       s3, binfo, ctab, ltab, hhdr, cstat, err, 0u);
     if (ev) (void)hipEventRecord(ev[1], st);
     hipLaunchKernelGGL(k_block_layout, dim3((L.nblocks + 63) / 64), dim3(64), 0, st, L.nblocks, binfo);
     if (ev) (void)hipEventRecord(ev[2], st);

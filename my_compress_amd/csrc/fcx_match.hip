@@ -1028,7 +1028,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     const uint32_t lo = b0 + (sn & 0xFFFFu);
                     const uint32_t n = ((sn >> 16) == 0xFFFFu ? b1 : min(b1, b0 + (sn >> 16))) - lo;
                     xpk[u] = x | (cap << 13) | ((h & 7u) << 22);   // bits 25..31: extension count
-                    if (n > kMaxChainSteps) rng[u] = 0xFFFFFFFFu;
+                    if (dbg & (1u << 22)) rng[u] = lo;   // (timing: setup only, no candidates)
+                    else if (n > kMaxChainSteps) rng[u] = 0xFFFFFFFFu;
                     else { rng[u] = lo | (n << 16); nmax = max(nmax, n); }
                 }
             }

@@ -1075,6 +1075,7 @@ void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_
     hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, mtok,
                        tile_off, tconv, binfo, s_flags, s_p, s_golomb, bhist);
     if (ev) (void)hipEventRecord(ev[0], st);
+    emit_dbg &= 0xFFFFu;   // (bits 16.. are k_tree's)
     if (emit_dbg == 0)
         hipLaunchKernelGGL(k_emit<false>, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok,
                            tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, bhist, 0u);
