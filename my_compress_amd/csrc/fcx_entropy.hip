@@ -106,6 +106,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
     __shared__ __attribute__((aligned(16))) uint32_t w[256];
     __shared__ uint32_t sw[257], ss[257], ln[256];   // (the merge reads the leaf queue two deep)
     __shared__ uint32_t iw[256], il[256], ir[256], par[512];
+    __shared__ __attribute__((aligned(16))) uint32_t sk[256];
     __shared__ uint32_t part[kTreeW][256];
     __shared__ uint32_t s_red[kTreeW];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -167,21 +168,25 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
 #pragma unroll
     for (uint32_t u = 0; u < 256 / kTreeT; u++) nz += w[tid + kTreeT * u] != 0 ? 1u : 0u;
     const uint32_t real = (uint32_t)__syncthreads_count(nz >= 1) + (uint32_t)__syncthreads_count(nz >= 2);
-    // stable sort of the leaves by (weight, symbol): rank = number of smaller keys
+    // stable sort of the leaves by (weight, symbol): rank = number of smaller keys.  A weight is at
+    // most the block size (<= 2^20 symbols), so weight << 8 | symbol fits 32 bits
 #pragma unroll
     for (uint32_t u = 0; u < 256 / kTreeT; u++) {
         const uint32_t sym = tid + kTreeT * u, wt = w[sym];
-        if (wt) {
-            const uint64_t key = ((uint64_t)wt << 8) | sym;
-            uint32_t rank = 0;
-            for (uint32_t j = 0; j < 256; j += 4) {
-                const uint4 w4 = *(const uint4 *)&w[j];
-                const uint32_t wj[4] = {w4.x, w4.y, w4.z, w4.w};
+        sk[sym] = wt ? (wt << 8) | sym : 0xFFFFFFFFu;
+    }
+    __syncthreads();
 #pragma unroll
-                for (uint32_t v = 0; v < 4; v++)
-                    rank += (wj[v] != 0 && (((uint64_t)wj[v] << 8) | (j + v)) < key) ? 1u : 0u;
+    for (uint32_t u = 0; u < 256 / kTreeT; u++) {
+        const uint32_t sym = tid + kTreeT * u, key = sk[sym];
+        if (key != 0xFFFFFFFFu) {
+            uint32_t rank = 0;
+#pragma unroll 4
+            for (uint32_t j = 0; j < 256; j += 4) {
+                const uint4 k4 = *(const uint4 *)&sk[j];
+                rank += (k4.x < key ? 1u : 0u) + (k4.y < key ? 1u : 0u) + (k4.z < key ? 1u : 0u) + (k4.w < key ? 1u : 0u);
             }
-            sw[rank] = wt;
+            sw[rank] = key >> 8;
             ss[rank] = sym;
         }
     }
