@@ -7,11 +7,15 @@ Metric (BASELINE.json): compress MB/s on 1 GB synthetic bytes at 1/2/4/8 MI355X;
 Headline (default, `scaling: strong`): ONE 1 GiB input (--global-mib) split into
 contiguous block ranges over the N ranks.  A timed step is the
 whole job: every rank compresses its device-resident shard into [u32 len][payload]
-records in HBM, the segment sizes are all-gathered, and the segments are
-concatenated in rank order into one contiguous stream on rank 0 (--concat gather:
-grouped point-to-point receives over all xGMI links; `allgather`: every rank gets
-the stream, one broadcast per source rank).  `value` = global input bytes x K /
-the max-over-ranks time of K such steps.  At N=1 there is nothing to concatenate.
+records in HBM and the segments end up concatenated in rank order in one contiguous
+stream on rank 0.  --concat pipe (default): the gather-aware partition (rank 0, the
+receiver, takes a larger block range, --share0, by default the share the step model
+of my_compress_amd.dist picks) and fcx_dist_compress_gather: the peers compress in
+--nsub pieces and send each piece over their xGMI link while the next compresses,
+rank 0 compresses its range meanwhile.  --concat gather: even split, compress, then a
+sizes all-gather and grouped point-to-point receives; `allgather`: every rank gets
+the stream, one broadcast per source rank.  `value` = global input bytes x K / the
+max-over-ranks time of K such steps.  At N=1 there is nothing to concatenate.
 The compress-only rate (no exchange) is reported beside it.  The assembled stream
 is checked against the reference's SHA-256 (HL-rand / HL-text / C3 / C5 digests,
 SURVEY.md §8(c)) at every N.
@@ -121,13 +125,20 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     import my_compress_amd as mc
     from my_compress_amd import dist as fdist
 
+    concat = args.concat if dist else "none"
+    share0 = 0
     if scaling == "strong":
         n_global = (global_mib or args.global_mib) << 20
-        lo, hi = fdist.byte_range(n_global, block, rank, world)
+        if concat == "pipe" and world > 1:   # the gather-aware partition
+            share0 = args.share0_ppm if args.share0_ppm >= 0 else fdist.gather_share_ppm(
+                world, kind, args.link_gbps, args.nsub)
+        ranges = [fdist.byte_range(n_global, block, r, world, share0) for r in range(world)]
     else:
         per = args.mib << 20
         n_global = per * world
-        lo, hi = rank * per, (rank + 1) * per
+        ranges = [(r * per, (r + 1) * per) for r in range(world)]
+    lo, hi = ranges[rank]
+    rank_bytes = [b - a for a, b in ranges]
     n = hi - lo
     t = time.time()
     if scaling == "weak" and kind != "rand":
@@ -140,9 +151,11 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     if world == 1 and args.host_path and main_leg:
         host_path = host_leg(host, n, block)
     del host
-    concat = args.concat if dist else "none"
-    # gather: rank 0's compress output buffer is also the file buffer (its segment sits at offset 0)
-    cap = mc.shard_bound(n_global if (concat == "gather" and rank == 0) else n, block)
+    # gather / pipe: rank 0's compress output buffer is also the file buffer (its segment sits at
+    # offset 0); pipe: a peer's pieces sit at their bound offsets
+    cap = mc.shard_bound(n_global if (concat in ("gather", "pipe") and rank == 0) else n, block)
+    if concat == "pipe" and rank != 0:
+        cap = mc.dist_gather_bound(n, block, args.nsub)
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     whole = None
     if concat == "allgather":
@@ -155,7 +168,34 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
         if n:
             ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid, sync=False)
 
+    def pieces():   # torch pipe path, a peer: its sub-batches compressed one by one as they are sent
+        o = 0
+        for a, b in fdist.piece_ranges(n, block, args.nsub):
+            pb = mc.shard_bound(b - a, block)
+            got = ctx.compress_shard(d_in.data_ptr() + a, b - a, d_out.data_ptr() + o, pb, sid) if b > a else 0
+            seg = d_out[o:o + got]
+            yield seg.cpu() if dist.get_backend() == "gloo" else seg
+            o += (pb + 15) // 16 * 16
+
     def step():   # the whole job: compress, sizes, concatenation in rank order
+        if concat == "pipe":
+            if args.fcx_dist is not None:   # C++ RCCL path: compress and gather overlapped
+                state["total"] = args.fcx_dist.compress_gather(ctx, d_in.data_ptr(), n, rank_bytes, args.nsub,
+                                                               d_out.data_ptr(), cap, sid)
+                return
+            gloo = dist.get_backend() == "gloo"
+            if rank == 0:
+                own = d_out[:ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid)] if n else d_out[:0]
+                if gloo:   # rehearsal without RCCL: the pieces travel through host memory
+                    hout = torch.empty(cap, dtype=torch.uint8)
+                    tot = fdist.compress_gather(None, dist, rank_bytes, block, args.nsub, own=own.cpu(), out=hout)
+                    d_out[:tot].copy_(hout[:tot])
+                else:
+                    tot = fdist.compress_gather(None, dist, rank_bytes, block, args.nsub, own=own, out=d_out)
+                state["total"] = tot
+            else:
+                state["total"] = fdist.compress_gather(pieces(), dist, rank_bytes, block, args.nsub)
+            return
         compress()
         seg_len = ctx.read_out_len() if n else 0
         if concat == "none":
@@ -216,14 +256,24 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     }
     if concat != "none":
         res["concat_ms_per_step"] = res["ms_per_step"] - res["compress_only"]["ms_per_step"]
-        res["concat_impl"] = "fcx_dist (C++ RCCL)" if args.fcx_dist is not None else \
-            f"torch.distributed ({dist.get_backend()})"
+        res["concat_impl"] = ("fcx_dist (C++ RCCL)" if args.fcx_dist is not None else
+                              f"torch.distributed ({dist.get_backend()})")
+        res["partition"] = {"share0_ppm": share0, "rank_bytes": rank_bytes,
+                            "nsub": args.nsub if concat == "pipe" else None}
+        if concat == "pipe" and scaling == "strong":
+            res["partition"]["model_ms"] = fdist.step_model_ms(
+                (share0 / 1e6) if share0 else 1.0 / world, world, fdist.COMPRESS_MS_PER_GIB.get(kind, 14.1),
+                fdist.RATIO.get(kind, 1.0), args.link_gbps, args.nsub, gib=n_global / GiB)
+            res["partition"]["model_link_gbps"] = args.link_gbps
     stats = ctx.stats() if n else {"tokens": 0, "matches": 0, "lazy_evals": 0, "lazy_tiles": 0}
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
     if not args.no_verify:
         res.update(verify(kind, seed, block, n_global, scaling, rank, world, dev, dist, d_out, whole, concat,
                           seg_len, total))
+    if concat == "pipe" and n:   # (a peer's pieces sit at their bound offsets: its own records again)
+        compress()
+        seg_len = ctx.read_out_len()
     if not args.no_decode and (main_leg or world == 1):
         res["decode"] = decode_leg(d_out, seg_len, n, block, d_in, args, dev, dist, world)
     ctx.close()
@@ -241,6 +291,20 @@ def verify(kind, seed, block, n_global, scaling, rank, world, dev, dist, d_out, 
     import my_compress_amd as mc
 
     out = {}
+    if scaling == "weak" and kind == "rand" and seed == 4 and n_global // world == GiB and concat == "pipe":
+        # the segments arrive concatenated on rank 0: each rank's slice against SURVEY.md B.3
+        oks = []
+        if rank == 0:
+            off = 0
+            for r in range(world):
+                want_bytes, want_prefix = inputs.C4_SEGMENTS[r] if r < len(inputs.C4_SEGMENTS) else (-1, "")
+                h = hashlib.sha256(memoryview(d_out[off:off + want_bytes].cpu().numpy())).hexdigest()
+                oks.append(int(want_bytes > 0 and off + want_bytes <= total and h[:16] == want_prefix))
+                off += max(want_bytes, 0)
+            oks[-1] &= int(off == total)
+            out["rank_segments_bit_exact"] = oks
+            out["bit_exact_vs_reference"] = all(oks)
+        return out
     if scaling == "weak" and kind == "rand" and seed == 4 and n_global // world == GiB:
         ok = 0
         if rank < len(inputs.C4_SEGMENTS):
@@ -262,7 +326,7 @@ def verify(kind, seed, block, n_global, scaling, rank, world, dev, dist, d_out, 
     key = (kind, seed, n_global, block)
     if key not in HL_DIGEST or rank != 0:
         return out
-    stream = d_out if concat in ("none", "gather") else whole
+    stream = d_out if concat in ("none", "gather", "pipe") else whole
     h = hashlib.sha256(mc.write_header(n_global, (n_global + block - 1) // block))
     h.update(memoryview(stream[:total].cpu().numpy()))
     want_sha, want_bytes = HL_DIGEST[key]
@@ -512,7 +576,14 @@ def main():
     ap.add_argument("--legs", default="c2,text,c3,zeros,runs,dna",
                     help="extra legs after the main one (comma list of " + ",".join(LEGS) + ")")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling (config 4) leg at N > 1")
-    ap.add_argument("--concat", default="gather", choices=["gather", "allgather", "none"])
+    ap.add_argument("--concat", default="pipe", choices=["pipe", "gather", "allgather", "none"],
+                    help="pipe: gather-aware partition, compress and gather overlapped (fcx_dist_compress_gather); "
+                         "gather: even split, compress, then gather to rank 0; allgather: the stream on every rank")
+    ap.add_argument("--share0", dest="share0_ppm", type=int, default=-1,
+                    help="pipe: rank 0's share of the blocks in ppm (-1 = the step model's choice)")
+    ap.add_argument("--nsub", type=int, default=4, help="pipe: sub-batches per peer")
+    ap.add_argument("--link-gbps", type=float, default=64.0,
+                    help="pipe: xGMI GB/s per link and direction assumed by the partition model")
     ap.add_argument("--concat-impl", default="fcx", choices=["fcx", "torch"],
                     help="fcx: the C++ RCCL path (fcx_dist_concat); torch: torch.distributed P2P / broadcast")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
@@ -605,8 +676,8 @@ def main():
                                    f"into one stream ({main_res['concat']})",
                        "kind": args.kind, "global_bytes": main_res["global_bytes"],
                        "bytes_per_gpu": n, "block_bytes": args.block,
-                       "parallelism": f"block-sharded x{world}, RCCL {main_res['concat']}" if world > 1
-                       else "single GPU"},
+                       "parallelism": (f"block-sharded x{world}, {main_res['concat']} over "
+                                       f"{main_res.get('concat_impl')}" if world > 1 else "single GPU")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "ratio": main_res["ratio"],
@@ -614,6 +685,7 @@ def main():
             "compress_only": main_res["compress_only"],
             "concat_ms_per_step": main_res.get("concat_ms_per_step"),
             "concat_impl": main_res.get("concat_impl"),
+            "partition": main_res.get("partition"),
             "stages_ms": main_res["stages_ms"],
             "lazy_evals": main_res["lazy_evals"],
             "decode": main_res.get("decode"),
@@ -622,7 +694,8 @@ def main():
         if world == 1 and not args.no_lz78 and not args.no_text:
             line["lz78"] = lz78_leg(dev)
         keep = ["value", "ms_per_step", "compress_only", "concat_ms_per_step", "ratio", "block_bytes", "stages_ms",
-                "lazy_evals", "lazy_tiles", "decode", "bit_exact_vs_reference", "global_bytes"]
+                "lazy_evals", "lazy_tiles", "decode", "bit_exact_vs_reference", "global_bytes", "partition",
+                "concat_impl"]
         for name, lr in legs.items():
             line[name] = {k: lr[k] for k in keep if k in lr}
         if weak is not None:

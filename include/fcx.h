@@ -222,6 +222,11 @@ typedef struct fcx_dist fcx_dist;
 
 /* contiguous block range [b0, b1) of rank r of n (the partition of my_compress_amd.dist) */
 void fcx_dist_block_range(uint64_t nblocks, int rank, int nranks, uint64_t *b0, uint64_t *b1);
+/* gather-aware partition: rank 0 (the receiver) takes floor(nblocks * share0_ppm / 10^6)
+ * blocks first, ranks 1..N-1 split the rest near-evenly (share0_ppm 0 = the even split
+ * above).  Equals my_compress_amd.dist.block_range(nblocks, rank, N, share0_ppm). */
+void fcx_dist_block_range_w(uint64_t nblocks, int rank, int nranks, uint32_t share0_ppm, uint64_t *b0,
+                            uint64_t *b1);
 /* a fresh RCCL unique id (rank 0 creates it; the caller hands it to every rank) */
 int fcx_dist_unique_id(uint8_t *id);
 /* one rank of an N-process job (one process per GPU, on HIP device `device`) */
@@ -238,6 +243,25 @@ int fcx_dist_size(fcx_dist *d, int *nranks, int *nlocal);
  * `stream` (a hipStream_t of the rank's device) and synchronised. */
 int fcx_dist_concat(fcx_dist *d, int local, const uint8_t *d_seg, uint64_t seg_len, uint8_t *d_out, uint64_t cap,
                     uint64_t *total, int mode, void *stream);
+/* The strong-scaling step of one rank, compress and concatenation overlapped (process-per-GPU
+ * form).  Every rank passes rank_bytes[0..N) (each rank's input bytes, e.g. from
+ * fcx_dist_block_range_w; the same array everywhere) and its own n = rank_bytes[rank] device
+ * bytes at d_in.  A peer (rank > 0) compresses its range as `nsub` sub-batches of whole blocks
+ * (1 <= nsub <= FCX_DIST_MAX_SUB), each at its bound offset of d_out (capacity >=
+ * fcx_dist_gather_bound(n, block, nsub)), and sends each piece to rank 0 as soon as it is done
+ * (its u64 length and error word, then its bytes) while the next piece compresses.  Rank 0
+ * compresses its range into d_out at offset 0 while the pieces arrive in a staging buffer the
+ * handle keeps, then moves them behind its own segment: d_out[0, *total) on rank 0 is every
+ * rank's [u32 len][payload] records in block order (capacity >= fcx_shard_bound of the whole
+ * input).  A peer whose compress fails sends failure words instead of pieces, so rank 0 always
+ * completes the exchange and returns the error.  *total: the concatenation on rank 0, the bytes
+ * sent on a peer.  Collective over the job; `stream` is the compress stream; returns after both
+ * streams are synchronised. */
+#define FCX_DIST_MAX_SUB 64u
+int fcx_dist_compress_gather(fcx_dist *d, fcx_ctx *ctx, const uint8_t *d_in, uint64_t n, const uint64_t *rank_bytes,
+                             uint32_t nsub, uint8_t *d_out, uint64_t cap, uint64_t *total, void *stream);
+/* d_out capacity fcx_dist_compress_gather needs for n input bytes in nsub sub-batches */
+uint64_t fcx_dist_gather_bound(uint64_t n, uint32_t block_bytes, uint32_t nsub);
 /* The whole job in one process (fcx_dist_init_local): host input, rounds of up to
  * round_bytes per device (0 = 1 GiB) split into block ranges, every device compresses
  * its range with one host thread each, the segments are gathered to local rank 0 over

@@ -105,6 +105,12 @@ def lib():
     P64 = ctypes.POINTER(ctypes.c_uint64)
     L.fcx_dist_block_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P64, P64]
     L.fcx_dist_block_range.restype = None
+    L.fcx_dist_block_range_w.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, P64, P64]
+    L.fcx_dist_block_range_w.restype = None
+    L.fcx_dist_gather_bound.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+    L.fcx_dist_gather_bound.restype = ctypes.c_uint64
+    L.fcx_dist_compress_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, P64,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, P64, ctypes.c_void_p]
     L.fcx_dist_unique_id.argtypes = [c_u8p]
     L.fcx_dist_init_rank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, c_u8p, ctypes.c_int]
     L.fcx_dist_init_local.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
@@ -418,11 +424,20 @@ def lz78_release() -> None:
 DIST_GATHER, DIST_ALLGATHER = 0, 1
 
 
-def dist_block_range(nblocks: int, rank: int, nranks: int):
-    """the C partition (fcx_dist_block_range); equals my_compress_amd.dist.block_range"""
+def dist_block_range(nblocks: int, rank: int, nranks: int, share0_ppm: int = 0):
+    """the C partition (fcx_dist_block_range, or fcx_dist_block_range_w with a rank-0 share);
+    equals my_compress_amd.dist.block_range"""
     b0, b1 = ctypes.c_uint64(), ctypes.c_uint64()
-    lib().fcx_dist_block_range(nblocks, rank, nranks, ctypes.byref(b0), ctypes.byref(b1))
+    if share0_ppm:
+        lib().fcx_dist_block_range_w(nblocks, rank, nranks, share0_ppm, ctypes.byref(b0), ctypes.byref(b1))
+    else:
+        lib().fcx_dist_block_range(nblocks, rank, nranks, ctypes.byref(b0), ctypes.byref(b1))
     return b0.value, b1.value
+
+
+def dist_gather_bound(n: int, block_bytes: int, nsub: int) -> int:
+    """a peer's d_out capacity for Dist.compress_gather (pieces at their bound offsets)"""
+    return int(lib().fcx_dist_gather_bound(n, block_bytes, nsub))
 
 
 def dist_unique_id() -> bytes:
@@ -473,6 +488,18 @@ class Dist:
         tot = ctypes.c_uint64()
         _check(lib().fcx_dist_concat(self._h, 0, ctypes.c_void_p(d_seg), seg_len, ctypes.c_void_p(d_out), cap,
                                      ctypes.byref(tot), mode, ctypes.c_void_p(stream)), "fcx_dist_concat")
+        return tot.value
+
+    def compress_gather(self, ctx: "Context", d_in: int, n: int, rank_bytes, nsub: int, d_out: int, cap: int,
+                        stream: int = 0) -> int:
+        """the strong-scaling step (fcx_dist_compress_gather): this rank compresses its n device
+        bytes (peers: in nsub pieces, each sent to rank 0 when done) and rank 0 ends with every
+        rank's records in block order at d_out; returns that length on rank 0, bytes sent elsewhere"""
+        rb = (ctypes.c_uint64 * len(rank_bytes))(*rank_bytes)
+        tot = ctypes.c_uint64()
+        _check(lib().fcx_dist_compress_gather(self._h, ctx._h, ctypes.c_void_p(d_in), n, rb, nsub,
+                                              ctypes.c_void_p(d_out), cap, ctypes.byref(tot),
+                                              ctypes.c_void_p(stream)), "fcx_dist_compress_gather")
         return tot.value
 
     def compress_host(self, data: bytes, block_bytes: int = BLOCK_BYTES, round_bytes: int = 0) -> bytes:

@@ -55,6 +55,13 @@ struct fcx_dist {
     std::vector<uint8_t *> din, dout;
     std::vector<hipStream_t> st;
     std::vector<uint64_t> dincap, dcap;
+    // fcx_dist_compress_gather's resources (process-per-GPU form), made on first use and kept
+    hipStream_t cst = nullptr;       // the exchange's stream (beside the caller's compress stream)
+    uint64_t *d_words = nullptr;     // 2 u64 per (sub-batch, rank): piece length, error bits
+    uint64_t *h_words = nullptr;     // pinned mirror
+    std::vector<hipEvent_t> ev;      // per sub-batch: compressed and its length copied
+    uint8_t *d_stage = nullptr;      // rank 0: the peers' pieces as they arrive
+    uint64_t stage_cap = 0;
 };
 
 namespace {
@@ -114,6 +121,65 @@ int concat_local(fcx_dist *d, int li, const uint8_t *d_seg, uint64_t seg_len, ui
     DHIP(hipStreamSynchronize(st));
     if (own != seg_len) return dfail(FCX_ERR_INTERNAL, "fcx_dist_concat: size exchange mismatch");
     return FCX_OK;
+}
+
+// fcx_dist_compress_gather's stream, length words and events (sized for FCX_DIST_MAX_SUB
+// sub-batches of every rank), and rank 0's staging buffer of at least `stage` bytes
+int ensure_gather(fcx_dist *d, uint64_t stage) {
+    DHIP(hipSetDevice(d->devices[0]));
+    const size_t words = 2ull * FCX_DIST_MAX_SUB * (size_t)d->nranks;
+    if (!d->cst) {
+        DHIP(hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking));
+        DHIP(hipMalloc((void **)&d->d_words, words * sizeof(uint64_t)));
+        DHIP(hipHostMalloc((void **)&d->h_words, words * sizeof(uint64_t), hipHostMallocDefault));
+        d->ev.assign(FCX_DIST_MAX_SUB, nullptr);
+        for (auto &e : d->ev) DHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (stage > d->stage_cap) {
+        if (d->d_stage) DHIP(hipFree(d->d_stage));
+        d->d_stage = nullptr;
+        d->stage_cap = 0;
+        if (hipMalloc((void **)&d->d_stage, stage) != hipSuccess)
+            return dfail(FCX_ERR_NOMEM, "fcx_dist_compress_gather: staging buffer of " + std::to_string(stage) + " B");
+        d->stage_cap = stage;
+    }
+    return FCX_OK;
+}
+
+void release_gather(fcx_dist *d) {
+    if (d->devices.empty()) return;
+    (void)hipSetDevice(d->devices[0]);
+    if (d->cst) (void)hipStreamSynchronize(d->cst);
+    for (auto e : d->ev)
+        if (e) (void)hipEventDestroy(e);
+    d->ev.clear();
+    if (d->cst) (void)hipStreamDestroy(d->cst);
+    if (d->d_words) (void)hipFree(d->d_words);
+    if (d->h_words) (void)hipHostFree(d->h_words);
+    if (d->d_stage) (void)hipFree(d->d_stage);
+    d->cst = nullptr; d->d_words = nullptr; d->h_words = nullptr; d->d_stage = nullptr; d->stage_cap = 0;
+}
+
+inline uint64_t round16(uint64_t x) { return (x + 15) & ~15ull; }
+
+// sub-batch s of nsub of a rank's n bytes: whole blocks, the near-even split of block_range
+void piece_range(uint64_t n, uint32_t block, uint32_t s, uint32_t nsub, uint64_t *lo, uint64_t *hi) {
+    const uint64_t nb = (n + block - 1) / block;
+    uint64_t b0, b1;
+    fcx_dist_block_range(nb, (int)s, (int)nsub, &b0, &b1);
+    *lo = b0 * block < n ? b0 * block : n;
+    *hi = b1 * block < n ? b1 * block : n;
+}
+
+// bytes a rank's pieces take at their bound offsets (a peer's d_out; rank 0's staging region)
+uint64_t pieces_bound(uint64_t n, uint32_t block, uint32_t nsub) {
+    uint64_t t = 0;
+    for (uint32_t s = 0; s < nsub; s++) {
+        uint64_t lo, hi;
+        piece_range(n, block, s, nsub, &lo, &hi);
+        t += round16(fcx_shard_bound(hi - lo, block));
+    }
+    return t;
 }
 
 void release_local(fcx_dist *d) {
@@ -177,6 +243,160 @@ void fcx_dist_block_range(uint64_t nblocks, int rank, int nranks, uint64_t *b0, 
     if (b1) *b1 = nblocks * (uint64_t)(rank + 1) / (uint64_t)nranks;
 }
 
+void fcx_dist_block_range_w(uint64_t nblocks, int rank, int nranks, uint32_t share0_ppm, uint64_t *b0,
+                            uint64_t *b1) {
+    // same arithmetic as my_compress_amd.dist.block_range(..., share0_ppm): rank 0 (the gather's
+    // receiver) takes floor(nblocks * ppm / 10^6) blocks, ranks 1..N-1 split the rest near-evenly
+    if (nranks <= 1 || share0_ppm == 0) { fcx_dist_block_range(nblocks, rank, nranks, b0, b1); return; }
+    const uint64_t ppm = share0_ppm > 1000000u ? 1000000u : share0_ppm;
+    const uint64_t n0 = (uint64_t)((unsigned __int128)nblocks * ppm / 1000000u);
+    uint64_t lo = 0, hi = n0;
+    if (rank > 0) {
+        uint64_t p0, p1;
+        fcx_dist_block_range(nblocks - n0, rank - 1, nranks - 1, &p0, &p1);
+        lo = n0 + p0;
+        hi = n0 + p1;
+    }
+    if (b0) *b0 = lo;
+    if (b1) *b1 = hi;
+}
+
+uint64_t fcx_dist_gather_bound(uint64_t n, uint32_t block_bytes, uint32_t nsub) {
+    if (block_bytes == 0) return 0;
+    if (nsub < 1) nsub = 1;
+    const uint64_t p = pieces_bound(n, block_bytes, nsub > FCX_DIST_MAX_SUB ? FCX_DIST_MAX_SUB : nsub);
+    const uint64_t w = fcx_shard_bound(n, block_bytes);
+    return p > w ? p : w;
+}
+
+int fcx_dist_compress_gather(fcx_dist *d, fcx_ctx *c, const uint8_t *d_in, uint64_t n, const uint64_t *rank_bytes,
+                             uint32_t nsub, uint8_t *d_out, uint64_t cap, uint64_t *total, void *stream) {
+    if (!d || !c || !rank_bytes || !total || !d_out || (n && !d_in) || nsub < 1 || nsub > FCX_DIST_MAX_SUB)
+        return dfail(FCX_ERR_ARG, "fcx_dist_compress_gather: bad argument");
+    if (d->comms.size() != 1)
+        return dfail(FCX_ERR_ARG, "fcx_dist_compress_gather: one rank per process (fcx_dist_init_rank)");
+    const int N = d->nranks, rank = d->base_rank;
+    if (rank_bytes[rank] != n) return dfail(FCX_ERR_ARG, "fcx_dist_compress_gather: rank_bytes[rank] != n");
+    int dev = 0;
+    uint32_t B = 0;
+    int rc = fcx_ctx_info(c, &dev, &B, nullptr);
+    if (rc) return rc;
+    if (dev != d->devices[0]) return dfail(FCX_ERR_ARG, "fcx_dist_compress_gather: context on another device");
+    hipStream_t st = (hipStream_t)stream;
+    ncclComm_t comm = d->comms[0];
+    *total = 0;
+    uint64_t stage = 0;
+    std::vector<uint64_t> soff(N, 0);   // rank 0: each peer's staging region
+    if (rank == 0)
+        for (int r = 1; r < N; r++) {
+            soff[r] = stage;
+            stage += pieces_bound(rank_bytes[r], B, nsub);
+        }
+    if ((rc = ensure_gather(d, stage))) return rc;
+    uint64_t *dw = d->d_words, *hw = d->h_words;
+    if (rank == 0) {
+        // own range straight into d_out at offset 0 (a failure is reported after the peers' pieces
+        // are drained, so no peer is left in a send), the peers' pieces into the staging regions
+        // on the exchange stream meanwhile: per round s, every peer's length words, then its bytes
+        int own_rc = fcx_compress_shard(c, d_in, n, d_out, cap, nullptr, st);
+        std::vector<uint64_t> fill(N, 0);
+        std::string peer_err;
+        for (uint32_t s = 0; s < nsub && N > 1; s++) {
+            uint64_t *ws = dw + 2ull * s * N, *hs = hw + 2ull * s * N;
+            DNCCL(ncclGroupStart());
+            for (int r = 1; r < N; r++) DNCCL(ncclRecv(ws + 2 * r, 2, ncclUint64, r, comm, d->cst));
+            DNCCL(ncclGroupEnd());
+            DHIP(hipMemcpyAsync(hs, ws, 2ull * N * sizeof(uint64_t), hipMemcpyDeviceToHost, d->cst));
+            DHIP(hipStreamSynchronize(d->cst));
+            DNCCL(ncclGroupStart());
+            for (int r = 1; r < N; r++) {
+                const uint64_t len = hs[2 * r], err = hs[2 * r + 1];
+                if (err || len == kFailed) {
+                    if (peer_err.empty()) peer_err = "rank " + std::to_string(r) + " failed in sub-batch " + std::to_string(s);
+                    continue;
+                }
+                if (len == 0) continue;
+                if (fill[r] + len > pieces_bound(rank_bytes[r], B, nsub))   // (bounded by construction)
+                    return dfail(FCX_ERR_INTERNAL, "fcx_dist_compress_gather: piece beyond its bound");
+                DNCCL(ncclRecv(d->d_stage + soff[r] + fill[r], len, ncclUint8, r, comm, d->cst));
+                fill[r] += len;
+            }
+            DNCCL(ncclGroupEnd());
+        }
+        DHIP(hipStreamSynchronize(d->cst));
+        uint64_t own = 0;
+        if (!own_rc) own_rc = fcx_ctx_read_out_len(c, &own);
+        if (own_rc) return own_rc;
+        if (!peer_err.empty()) return dfail(FCX_ERR_RCCL, "fcx_dist_compress_gather: " + peer_err);
+        uint64_t off = own;
+        for (int r = 1; r < N; r++) off += fill[r];
+        if (off > cap) return dfail(FCX_ERR_CAPACITY, "fcx_dist_compress_gather: output capacity too small (" +
+                                                          std::to_string(off) + " B)");
+        off = own;
+        for (int r = 1; r < N; r++) {   // the peers' bytes behind the own segment, in rank order
+            if (fill[r]) DHIP(hipMemcpyAsync(d_out + off, d->d_stage + soff[r], fill[r], hipMemcpyDeviceToDevice, st));
+            off += fill[r];
+        }
+        DHIP(hipStreamSynchronize(st));
+        *total = off;
+        return FCX_OK;
+    }
+    // a peer: every piece's compress is enqueued at once at its bound offset of d_out; each piece's
+    // length words follow it on the compress stream, and the exchange stream sends them and then
+    // the piece's bytes as soon as the piece is done, while the next piece compresses
+    std::vector<uint64_t> ro(nsub, 0), lens(nsub, 0);
+    int status = FCX_OK;
+    std::string msg;
+    uint64_t o = 0;
+    for (uint32_t s = 0; s < nsub; s++) {
+        uint64_t lo, hi;
+        piece_range(n, B, s, nsub, &lo, &hi);
+        ro[s] = o;
+        const uint64_t pb = round16(fcx_shard_bound(hi - lo, B));
+        if (status == FCX_OK && o + pb > cap) {
+            status = dfail(FCX_ERR_CAPACITY, "fcx_dist_compress_gather: peer output capacity too small (see fcx_dist_gather_bound)");
+            msg = fcx_last_error();
+        }
+        if (status == FCX_OK) {
+            status = fcx_compress_shard(c, d_in + lo, hi - lo, d_out + o, pb, nullptr, st);
+            if (status) msg = fcx_last_error();
+        }
+        if (status == FCX_OK) {
+            DHIP(hipMemcpyAsync(dw + 2 * s, fcx_ctx_device_out_len(c), 2 * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+            DHIP(hipMemcpyAsync(hw + 2 * s, dw + 2 * s, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            DHIP(hipEventRecord(d->ev[s], st));
+        }
+        o += pb;
+    }
+    uint64_t sent = 0;
+    for (uint32_t s = 0; s < nsub; s++) {
+        bool ok = status == FCX_OK && hipEventSynchronize(d->ev[s]) == hipSuccess;
+        if (ok && hw[2 * s + 1]) {
+            status = dfail(hw[2 * s + 1] & 4u ? FCX_ERR_CAPACITY : FCX_ERR_INTERNAL,
+                           "fcx_dist_compress_gather: device error bits " + std::to_string(hw[2 * s + 1]));
+            msg = fcx_last_error();
+            ok = false;
+        }
+        if (!ok) {   // publish the failure in this and every later round (rank 0 keeps the protocol)
+            if (status == FCX_OK) { status = dfail(FCX_ERR_HIP, "fcx_dist_compress_gather: compress failed"); msg = fcx_last_error(); }
+            hw[2 * s] = kFailed;
+            hw[2 * s + 1] = 1;
+            DHIP(hipMemcpyAsync(dw + 2 * s, hw + 2 * s, 2 * sizeof(uint64_t), hipMemcpyHostToDevice, d->cst));
+        } else {
+            lens[s] = hw[2 * s];
+            DHIP(hipStreamWaitEvent(d->cst, d->ev[s], 0));
+        }
+        DNCCL(ncclSend(dw + 2 * s, 2, ncclUint64, 0, comm, d->cst));
+        if (ok && lens[s]) DNCCL(ncclSend(d_out + ro[s], lens[s], ncclUint8, 0, comm, d->cst));
+        sent += lens[s];
+    }
+    DHIP(hipStreamSynchronize(d->cst));
+    DHIP(hipStreamSynchronize(st));
+    if (status) return dfail(status, msg);
+    *total = sent;
+    return FCX_OK;
+}
+
 int fcx_dist_unique_id(uint8_t *id) {
     if (!id) return dfail(FCX_ERR_ARG, "fcx_dist_unique_id: NULL");
     ncclUniqueId u;
@@ -225,6 +445,7 @@ int fcx_dist_init_local(fcx_dist **out, int ndev, const int *devices) {
 void fcx_dist_destroy(fcx_dist *d) {
     if (!d) return;
     release_local(d);
+    release_gather(d);
     for (size_t i = 0; i < d->comms.size(); i++) {
         (void)hipSetDevice(d->devices[i]);
         (void)hipDeviceSynchronize();

@@ -25,15 +25,70 @@ import torch
 from . import write_header
 
 
-def block_range(nblocks: int, rank: int, world: int):
-    """contiguous block range [b0, b1) of `rank`"""
-    return nblocks * rank // world, nblocks * (rank + 1) // world
+def block_range(nblocks: int, rank: int, world: int, share0_ppm: int = 0):
+    """contiguous block range [b0, b1) of `rank`.  share0_ppm = 0: the even split (sizes differ
+    by at most one block).  Otherwise the gather-aware split (fcx_dist_block_range_w): rank 0,
+    the receiver of the concatenation, takes nblocks * share0_ppm // 10^6 blocks first, and
+    ranks 1..N-1 split the rest evenly."""
+    world = max(world, 1)
+    if world == 1 or share0_ppm <= 0:
+        return nblocks * rank // world, nblocks * (rank + 1) // world
+    n0 = nblocks * min(share0_ppm, 1_000_000) // 1_000_000
+    if rank == 0:
+        return 0, n0
+    p0, p1 = block_range(nblocks - n0, rank - 1, world - 1)
+    return n0 + p0, n0 + p1
 
 
-def byte_range(n: int, block_bytes: int, rank: int, world: int):
+def byte_range(n: int, block_bytes: int, rank: int, world: int, share0_ppm: int = 0):
     nblocks = (n + block_bytes - 1) // block_bytes
-    b0, b1 = block_range(nblocks, rank, world)
+    b0, b1 = block_range(nblocks, rank, world, share0_ppm)
     return min(n, b0 * block_bytes), min(n, b1 * block_bytes)
+
+
+def piece_ranges(n: int, block_bytes: int, nsub: int):
+    """the nsub sub-batches of a rank's n bytes (whole blocks, near-even), as fcx_dist's piece_range"""
+    nb = (n + block_bytes - 1) // block_bytes
+    out = []
+    for s in range(nsub):
+        b0, b1 = block_range(nb, s, nsub)
+        out.append((min(n, b0 * block_bytes), min(n, b1 * block_bytes)))
+    return out
+
+
+# ---- the strong-scaling step model (DESIGN.md §6) --------------------------------------------
+# One GPU's compress time per GiB and output ratio for each synthetic kind at 1 MiB blocks
+# (bench.py on one MI355X, profiles/r03_bench_n1.json), the defaults of gather_share_ppm.
+COMPRESS_MS_PER_GIB = {"rand": 4.8, "text": 14.1, "zeros": 3.4, "runs": 12.0, "dna": 57.7}
+RATIO = {"rand": 1.0164, "text": 0.582, "zeros": 0.007, "runs": 0.0396, "dna": 0.27}
+
+
+def step_model_ms(share0: float, world: int, c_ms: float, ratio: float, link_gbps: float, nsub: int,
+                  gib: float = 1.0, copy_gbps: float = 2500.0):
+    """modelled ms of one gather step of `gib` GiB: rank 0 compresses share0 of the input while
+    each peer compresses (1 - share0) / (N - 1) of it in nsub pieces and sends each piece over its
+    own link as soon as it is done (pipeline: first piece, then the slower of compress and send per
+    piece, then the last send); rank 0 then moves the peers' bytes behind its segment (an HBM copy,
+    read + write at copy_gbps).  c_ms: one GPU's compress ms per GiB."""
+    if world <= 1:
+        return gib * c_ms
+    gp = (1.0 - share0) / (world - 1) * gib
+    a = gp * c_ms / nsub                                   # one piece's compress
+    b = gp * ratio * (1 << 30) / (link_gbps * 1e9) * 1e3 / nsub   # one piece's send
+    peer = a + (nsub - 1) * max(a, b) + b
+    copy = (1.0 - share0) * gib * ratio * (1 << 30) * 2 / (copy_gbps * 1e9) * 1e3
+    return max(share0 * gib * c_ms, peer) + copy
+
+
+def gather_share_ppm(world: int, kind: str = "rand", link_gbps: float = 64.0, nsub: int = 4,
+                     c_ms: float = None, ratio: float = None) -> int:
+    """rank 0's block share (ppm) that minimises step_model_ms; 0 (even split) for one rank"""
+    if world <= 1:
+        return 0
+    c_ms = COMPRESS_MS_PER_GIB.get(kind, 14.1) if c_ms is None else c_ms
+    ratio = RATIO.get(kind, 1.0) if ratio is None else ratio
+    best = min(range(1000, 1_000_000, 1000), key=lambda p: step_model_ms(p / 1e6, world, c_ms, ratio, link_gbps, nsub))
+    return best
 
 
 def exchange_sizes(seg_len: int, dist, device, group=None):
@@ -91,6 +146,73 @@ def allgather_segments(seg: torch.Tensor, out: torch.Tensor, sizes, offs, dist, 
     for w in works:
         w.wait()
     return sum(sizes)
+
+
+def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=None, out=None, group=None):
+    """fcx_dist_compress_gather's protocol over torch.distributed (the `--concat-impl torch` path
+    and the gloo tests).  A peer passes `pieces`, an iterable of its nsub sub-batch segments in
+    order (uint8 tensors, e.g. compressed one by one as they are consumed): each is sent as it is
+    produced, an int64 pair (length, error) first, then its bytes.  Rank 0 passes its own
+    segment `own` (already at out[:len], or copied there) and `out` (>= the whole
+    concatenation); per round s it receives every peer's length pair, then every peer's bytes
+    into a staging region per peer, and finally moves them behind its own segment in rank order.
+    A peer that fails sends (-1, 1) for this and every later round.  Returns the concatenated
+    length on rank 0, the bytes sent on a peer."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    dev = out.device if out is not None else torch.device("cpu")
+    if rank != 0:
+        sent, failed = 0, False
+        it = iter(pieces)
+        for s in range(nsub):
+            seg = None
+            if not failed:
+                try:
+                    seg = next(it)
+                except Exception:   # a failed compress: publish it, keep the protocol
+                    failed = True
+            n = 0 if failed else int(seg.numel())
+            words = torch.tensor([-1, 1] if failed else [n, 0], dtype=torch.int64, device=seg.device if seg is not None
+                                 else dev)
+            dist.send(words, 0, group)
+            if n:
+                dist.send(seg.contiguous(), 0, group)
+            sent += n
+        if failed:
+            raise RuntimeError("compress_gather: this rank's compress failed")
+        return sent
+    stage_cap = [0] + [sum(2 * (hi - lo) + 4096 * ((hi - lo + block_bytes - 1) // block_bytes) + 64
+                           for lo, hi in piece_ranges(rank_bytes[r], block_bytes, nsub)) for r in range(1, world)]
+    stage = [torch.empty(max(c, 1), dtype=torch.uint8, device=dev) for c in stage_cap]
+    fill = [0] * world
+    err = None
+    for s in range(nsub):
+        words = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
+        ops = [dist.P2POp(dist.irecv, words[r], r, group) for r in range(1, world)]
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        ops = []
+        for r in range(1, world):
+            n, e = int(words[r][0]), int(words[r][1])
+            if e or n < 0:
+                err = err or f"rank {r} failed in sub-batch {s}"
+                continue
+            if n:
+                ops.append(dist.P2POp(dist.irecv, stage[r][fill[r]:fill[r] + n], r, group))
+                fill[r] += n
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+    if err:
+        raise RuntimeError("compress_gather: " + err)
+    n_own = int(own.numel()) if own is not None else 0
+    _place_own(own if own is not None else torch.zeros(0, dtype=torch.uint8, device=dev), out, 0)
+    off = n_own
+    for r in range(1, world):
+        out[off:off + fill[r]].copy_(stage[r][:fill[r]])
+        off += fill[r]
+    return off
 
 
 def concat_segments(seg: torch.Tensor, dist, group=None, mode: str = "allgather", dst: int = 0):

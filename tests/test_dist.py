@@ -103,3 +103,118 @@ def test_dist_needs_a_gpu_without_one():
         pytest.skip("GPU present")
     with pytest.raises(mc.FcxError):
         mc.Dist.local([0])
+
+
+# ---- gather-aware partition + pipelined gather (fcx_dist_compress_gather's protocol) ----------
+def _gather_worker(rank, world, port, cases, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        for idx, (spec, block, share, nsub, fail_rank) in enumerate(cases):
+            data = inputs.make(spec)
+            rb = [(lambda lo_hi: lo_hi[1] - lo_hi[0])(fdist.byte_range(len(data), block, r, world, share))
+                  for r in range(world)]
+            lo, hi = fdist.byte_range(len(data), block, rank, world, share)
+            mine = data[lo:hi]
+
+            def pieces():   # each sub-batch compressed only when the protocol asks for it
+                for s, (a, b) in enumerate(fdist.piece_ranges(len(mine), block, nsub)):
+                    if rank == fail_rank and s == nsub - 1:
+                        raise RuntimeError("injected compress failure")
+                    seg = oracle.compress_file(mine[a:b], block)[10:] if b > a else b""
+                    yield torch.frombuffer(bytearray(seg), dtype=torch.uint8) if seg else torch.zeros(0, dtype=torch.uint8)
+
+            try:
+                if rank == 0:
+                    own = oracle.compress_file(mine, block)[10:] if mine else b""
+                    out = torch.zeros(2 * len(data) + 4096 * (len(data) // block + 2), dtype=torch.uint8)
+                    own_t = torch.frombuffer(bytearray(own), dtype=torch.uint8) if own else torch.zeros(0, dtype=torch.uint8)
+                    n = fdist.compress_gather(None, dist, rb, block, nsub, own=own_t, out=out)
+                    results[(idx, rank)] = fdist.assemble_file(len(data), block, out[:n].numpy().tobytes())
+                else:
+                    results[(idx, rank)] = fdist.compress_gather(pieces(), dist, rb, block, nsub)
+            except RuntimeError as e:
+                results[(idx, rank)] = "error: " + str(e)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_gather_uneven_partition(world):
+    """rank 0 takes a larger block range (the gather-aware split), the peers send their ranges in
+    sub-batches as they compress them; rank 0's assembled file equals the single-process oracle
+    file byte for byte.  A peer whose compress fails publishes it: rank 0 raises, nobody hangs."""
+    text = {"type": "gen", "kind": "text", "seed": 5, "n": 700000}
+    cases = [
+        (text, 65536, fdist.gather_share_ppm(world, "text"), 3, -1),
+        (text, 65536, 600000, 4, -1),                                      # peers get 1-3 pieces of blocks
+        ({"type": "mosaic", "seed": 9, "n": 333333}, 16384, 500000, 1, -1),
+        ({"type": "mosaic", "seed": 9, "n": 333333}, 16384, 0, 5, -1),     # even split, 5 pieces
+        ({"type": "gen", "kind": "rand", "seed": 1, "n": 70000}, 65536, 900000, 3, -1),   # peers (almost) empty
+        (text, 65536, 500000, 2, world - 1),                               # injected failure
+    ]
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_gather_worker, args=(world, _free_port(), cases, results), nprocs=world, join=True)
+    for idx, (spec, block, share, nsub, fail_rank) in enumerate(cases):
+        if fail_rank >= 0:
+            assert str(results[(idx, 0)]).startswith("error:") and "failed" in results[(idx, 0)], results[(idx, 0)]
+            assert str(results[(idx, fail_rank)]).startswith("error:")
+            continue
+        data = inputs.make(spec)
+        assert results[(idx, 0)] == oracle.compress_file(data, block), (idx, spec, share, nsub)
+
+
+def test_weighted_partition():
+    for nb in [0, 1, 2, 7, 1024, 8192]:
+        for world in [1, 2, 3, 4, 8]:
+            for ppm in [0, 1, 125000, 500000, 787000, 999999, 1000000]:
+                rs = [fdist.block_range(nb, r, world, ppm) for r in range(world)]
+                assert rs[0][0] == 0 and rs[-1][1] == nb
+                assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+                if world > 1 and ppm:
+                    assert rs[0][1] == nb * ppm // 1_000_000
+                    peers = [b - a for a, b in rs[1:]]
+                    assert max(peers) - min(peers) <= 1
+
+
+def test_c_weighted_partition_matches_python():
+    import my_compress_amd as mc
+
+    for nb in [0, 1, 5, 1024, 8192, 65535]:
+        for world in [1, 2, 3, 8]:
+            for ppm in [0, 333333, 787000, 1000000]:
+                for r in range(world):
+                    assert mc.dist_block_range(nb, r, world, ppm) == fdist.block_range(nb, r, world, ppm)
+
+
+def test_piece_ranges_cover_in_block_order():
+    for n, block, nsub in [(0, 4096, 3), (1, 4096, 4), (10 * 4096 + 5, 4096, 4), (1 << 20, 65536, 64)]:
+        pr = fdist.piece_ranges(n, block, nsub)
+        assert len(pr) == nsub and pr[0][0] == 0 and pr[-1][1] == n
+        assert all(pr[i][1] == pr[i + 1][0] for i in range(nsub - 1))
+        assert all(a % block == 0 for a, _ in pr)
+
+
+def test_gather_bound_holds_pieces():
+    import my_compress_amd as mc
+
+    for n, block, nsub in [(0, 1 << 20, 4), (5 << 20, 1 << 20, 4), (123456789, 1 << 16, 64), (1 << 30, 1 << 20, 8)]:
+        want = sum((mc.shard_bound(hi - lo, block) + 15) // 16 * 16 for lo, hi in fdist.piece_ranges(n, block, nsub))
+        assert mc.dist_gather_bound(n, block, nsub) >= max(want, mc.shard_bound(n, block))
+
+
+def test_step_model_is_monotone_by_design():
+    """the gather-aware split keeps the modelled strong-scaling step (1 GiB, gather to rank 0,
+    64 GB/s per xGMI link, 4 pieces) below the one-GPU step at every N, for rand and text"""
+    for kind in ("rand", "text"):
+        c, r = fdist.COMPRESS_MS_PER_GIB[kind], fdist.RATIO[kind]
+        t = [fdist.step_model_ms(fdist.gather_share_ppm(n, kind) / 1e6 if n > 1 else 1.0, n, c, r, 64.0, 4)
+             for n in (1, 2, 4, 8)]
+        assert t[0] > t[1] > t[2] > t[3], (kind, t)
+        # the even split with one send at the end (round 3's step) is slower than one GPU at N = 2
+        even = fdist.step_model_ms(0.5, 2, c, r, 64.0, 1)
+        if kind == "rand":
+            assert even > t[0]

@@ -79,3 +79,30 @@ def test_cli_gpus_flag_matches_single_device(tmp_path, golden):
     one, dist = (tmp_path / "one").read_bytes(), (tmp_path / "dist").read_bytes()
     assert one == dist
     assert hashlib.sha256(dist).hexdigest() == case["out_sha256"]
+
+
+def test_rank_compress_gather_one_rank(cuda):
+    """fcx_dist_compress_gather on a one-rank communicator: the compress + exchange step of the
+    strong-scaling bench (no peers: rank 0's own range, every nsub) equals the reference file"""
+    import torch
+
+    d = mc.Dist.rank(1, 0, mc.dist_unique_id(), 0)
+    ctx = mc.Context(0, 65536, 1 << 20)
+    try:
+        data = inputs.make({"type": "mosaic", "seed": 31, "n": 700001})
+        want = oracle.compress_file(data, 65536)
+        d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
+        cap = mc.shard_bound(len(data), 65536)
+        out = torch.zeros(cap, dtype=torch.uint8, device=cuda)
+        st = torch.cuda.current_stream().cuda_stream
+        for nsub in (1, 4, 64):
+            out.zero_()
+            n = d.compress_gather(ctx, d_in.data_ptr(), len(data), [len(data)], nsub, out.data_ptr(), cap, st)
+            assert mc.write_header(len(data), 11) + out[:n].cpu().numpy().tobytes() == want
+        with pytest.raises(mc.FcxError):   # rank_bytes[rank] must be this rank's n
+            d.compress_gather(ctx, d_in.data_ptr(), len(data), [len(data) - 1], 1, out.data_ptr(), cap, st)
+        with pytest.raises(mc.FcxError):   # nsub out of range
+            d.compress_gather(ctx, d_in.data_ptr(), len(data), [len(data)], 65, out.data_ptr(), cap, st)
+    finally:
+        ctx.close()
+        d.close()
