@@ -438,16 +438,18 @@ def host_cpu_share():
     return aff, f"sched_getaffinity: {aff} CPUs (no cgroup quota)"
 
 
-def cpu_baseline(kind, seed, block, threads=None, nblocks=None, nblocks_1t=8):
+def cpu_baseline(kind, seed, block, threads=None, nblocks=None, nblocks_1t=8, mib_per_thread=8, mib_1t=8):
     """the reference's block encoder (oracle/_ref, compiled from /root/reference) on
-    the first nblocks blocks of the same shard, one host thread per CPU of this
-    process's share (host_cpu_share), plus the first nblocks_1t blocks on one thread
-    (the reference is single-threaded)"""
+    the first nblocks blocks of the same shard (default: mib_per_thread MiB per thread),
+    one host thread per CPU of this process's share (host_cpu_share), plus the first
+    nblocks_1t blocks (default: mib_1t MiB) on one thread (the reference is single-threaded)"""
     import oracle
 
     share, share_how = host_cpu_share()
     threads = threads or share
-    nblocks = nblocks or min(256, 8 * threads)   # ~10-60 s of CPU work at 0.5-1 s per 1 MiB block
+    per_thread = max(1, (mib_per_thread << 20) // block)
+    nblocks = nblocks or min(256 * max(1, (1 << 20) // block), per_thread * threads)
+    nblocks_1t = min(nblocks, max(nblocks_1t if block >= (1 << 20) else 0, (mib_1t << 20) // block, 1))
 
     R = oracle.ref()
     kind_used = "reference"
@@ -554,6 +556,30 @@ def lz78_leg(dev, mib=1024, block=1 << 20, reps=2, ref_blocks=2):
                              "sample": f"first {ref_blocks} x {block // 1024} KiB blocks, my_compress_file_lz78"}}
 
 
+def roofline(res, pmc_leg, pmc):
+    """roofline of a leg's dominant kernel (largest hipEvent stage time over the K compress-only
+    steps): achieved = the leg's algorithmic bytes on this rank (input + compressed
+    output, 1 + r per input byte) / that kernel's average time; traffic = FETCH_SIZE x 2 + WRITE_SIZE
+    per launch from the committed PMC summary for this leg (`pmc_leg`:stage), scaled to this shard"""
+    stages = {k: v for k, v in res["stages_ms"].items() if k != "memset"}
+    dom = max(stages, key=stages.get) if stages else None
+    n = res["bytes_this_rank"]
+    alg = n + res["seg_bytes_rank0"]
+    achieved = alg / (stages[dom] * 1e-3) / 1e9 if dom else None
+    traffic = None
+    key = f"{pmc_leg}:{dom}"
+    if pmc_leg and key in pmc:   # PMC passes ran on a whole 1 GiB shard; scale to this rank's launch
+        traffic = pmc[key].get("hbm_bytes_per_launch") * n / pmc[key].get("input_bytes", GiB)
+    return {"bound": "hbm", "kernel": f"k_{dom}" if dom else None, "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+            "alg_bytes_per_launch": alg, "kernel_ms": stages.get(dom),
+            "note": "achieved = (this rank's input + its compressed segment) / the dominant kernel's average "
+                    "hipEvent time over the K compress-only steps; traffic = FETCH_SIZE x 2 + WRITE_SIZE per "
+                    "launch from profiles/pmc_latest.json (rocprofv3 PMC passes), scaled to this shard",
+            "path_achieved": alg / (res["compress_only"]["ms_per_step"] * 1e-3) / 1e9,
+            "path_frac": alg / (res["compress_only"]["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def load_pmc(path):
     if path and os.path.exists(path):
         with open(path) as f:
@@ -640,28 +666,16 @@ def main():
         weak = run_leg("rand", 4, 1 << 20, args, rank, world, dev, dist, False, scaling="weak")
 
     if rank == 0:
-        stages = {k: v for k, v in main_res["stages_ms"].items() if k != "memset"}
-        dom = max(stages, key=stages.get) if stages else None
-        n = main_res["bytes_this_rank"]
-        alg = n + main_res["seg_bytes_rank0"]     # 1 + r bytes per input byte, this rank's launch
-        achieved = alg / (stages[dom] * 1e-3) / 1e9 if dom else None
         pmc = load_pmc(args.pmc)
-        traffic = None
-        key = f"{args.kind}:{dom}"
-        if key in pmc:   # PMC passes ran on a whole 1 GiB shard; scale to this rank's launch
-            t_in = pmc[key].get("input_bytes", GiB)
-            traffic = pmc[key].get("hbm_bytes_per_launch") * n / t_in
-        roof = {"bound": "hbm", "kernel": f"k_{dom}" if dom else None, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "alg_bytes_per_launch": alg,
-                "note": "achieved = (rank-0 shard input + its compressed segment) / k_match's average hipEvent "
-                        "time over the K compress-only steps; traffic = FETCH_SIZE x 2 + WRITE_SIZE per launch "
-                        "from profiles/pmc_latest.json (rocprofv3 PMC passes), scaled to this shard",
-                "path_achieved": alg / (main_res["compress_only"]["ms_per_step"] * 1e-3) / 1e9}
+        n = main_res["bytes_this_rank"]
+        roof = roofline(main_res, args.kind if args.block == 1 << 20 else None, pmc)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.kind, SEEDS[args.kind], args.block)
-        shard_note = "the whole input" if world == 1 else f"1/{world} of it per rank (contiguous block ranges)"
+        part = main_res.get("partition") or {}
+        shard_note = "the whole input" if world == 1 else (
+            f"contiguous block ranges over {world} ranks" +
+            (f", rank 0 (the receiver) {part['share0_ppm'] / 1e4:.1f} %" if part.get("share0_ppm") else ", even"))
         line = {
             "metric": METRIC, "value": main_res["value"], "unit": "MB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": main_res["ms_per_step"],
@@ -698,6 +712,11 @@ def main():
                 "concat_impl"]
         for name, lr in legs.items():
             line[name] = {k: lr[k] for k in keep if k in lr}
+            line[name]["roofline"] = roofline(lr, name, pmc)
+            if world == 1 and not args.no_cpu_baseline:   # a smaller sample per extra leg: ~2 MiB per thread
+                kind, block = LEGS[name][:2]
+                seed = LEGS[name][2] if len(LEGS[name]) > 2 else SEEDS[kind]
+                line[name]["cpu_baseline"] = cpu_baseline(kind, seed, block, mib_per_thread=2, mib_1t=2)
         if weak is not None:
             line["weak"] = {k: weak[k] for k in keep + ["rank_segments_bit_exact", "global_bytes"] if k in weak}
             line["weak"]["workload"] = (f"BASELINE config 4 sharding: rank r = bytes [r GiB, (r+1) GiB) of the "
