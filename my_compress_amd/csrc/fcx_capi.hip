@@ -19,14 +19,13 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev,
-                  uint32_t emit_dbg = 0);
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *sdesc, hipStream_t st,
+                  hipEvent_t *ev, uint32_t emit_dbg = 0);
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
-                    const uint16_t *thist, const uint32_t *bhist, const uint32_t *tile_off, uint32_t *ctab,
+                    const uint16_t *thist, uint32_t *ctab,
                     uint8_t *ltab, uint8_t *hhdr, uint64_t *cstat, uint64_t *blk_off, uint64_t *total, uint8_t *out,
-                    uint64_t cap, uint32_t *err, hipStream_t st, hipEvent_t *ev, hipEvent_t wait_scan,
-                    hipEvent_t rec_scan,
-                    uint32_t tree_dbg = 0);
+                    uint64_t cap, uint32_t *err, const uint8_t *in, const uint32_t *sdesc, hipStream_t st, hipEvent_t *ev,
+                    hipEvent_t wait_scan, hipEvent_t rec_scan, uint32_t tree_dbg = 0);
 }  // namespace fcx
 
 using namespace fcx;
@@ -101,8 +100,8 @@ struct fcx_ctx {
     BlockInfo *binfo = nullptr;
     uint8_t *s[kStreams] = {nullptr, nullptr, nullptr, nullptr};
     uint16_t *thist = nullptr;         // per tile: chars counts (k_emit)
-    uint32_t *bhist = nullptr;         // per block: 256 bins of each stream (k_emit; flags, distances, golomb)
     uint64_t *cstat = nullptr;         // per chunk: k_encode's look-back status word
+    uint32_t *sdesc = nullptr;         // per 64 chars: run of input bytes (offset) or kCdMixed (k_emit)
     uint32_t *ctab = nullptr;          // code table
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
@@ -129,7 +128,7 @@ struct fcx_ctx {
 namespace {
 void free_scratch(fcx_ctx *c) {
     void *ptrs[] = {c->m,    c->mbits, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->mtok, c->tconv, c->fp, c->binfo,
-                    c->s[0], c->s[1],  c->s[2],      c->s[3],       c->thist,    c->bhist,    c->cstat,
+                    c->s[0], c->s[1],  c->s[2],      c->s[3],       c->thist,    c->cstat, c->sdesc,
                     c->ctab, c->ltab,  c->hhdr,      c->blk_off};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -137,7 +136,7 @@ void free_scratch(fcx_ctx *c) {
     c->mtok = c->tconv = nullptr;
     c->binfo = nullptr;
     for (auto &p : c->s) p = nullptr;
-    c->thist = nullptr; c->bhist = nullptr; c->cstat = nullptr; c->ctab = nullptr;
+    c->thist = nullptr; c->cstat = nullptr; c->sdesc = nullptr; c->ctab = nullptr;
     c->ltab = c->hhdr = nullptr;
     c->blk_off = nullptr;
     c->cap_n = 0;
@@ -170,8 +169,8 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     for (uint32_t s = 0; s < kStreams; s++)
         if ((r = dalloc(&c->s[s], (uint64_t)L.sstride[s] * nb + 64, "stream"))) return r;
     if ((r = dalloc(&c->thist, 2ull * 256 * nt, "thist"))) return r;
-    if ((r = dalloc(&c->bhist, 4ull * 256 * kStreams * nb, "bhist"))) return r;
     if ((r = dalloc(&c->cstat, 16ull * L.cpb_total * nb, "cstat"))) return r;
+    if ((r = dalloc(&c->sdesc, 4ull * ((c->B + kCharSeg - 1) / kCharSeg) * nb, "sdesc"))) return r;
     if ((r = dalloc(&c->ctab, 4ull * 256 * kStreams * nb, "ctab"))) return r;
     if ((r = dalloc(&c->ltab, 256ull * kStreams * nb, "ltab"))) return r;
     if ((r = dalloc(&c->hhdr, (uint64_t)kHuffHdrStride * kStreams * nb, "hhdr"))) return r;
@@ -364,16 +363,18 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         launch_parse(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
                      c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 12 * t0,
                      c->tile_off + 3 * t0, c->tconv + t0, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3],
-                     c->thist + t0 * 256, c->bhist + b0 * kStreams * 256, sg, ev ? ev + 3 : nullptr, c->emit_dbg);
+                     c->thist + t0 * 256, c->sdesc + b0 * ((c->B + kCharSeg - 1) / kCharSeg), sg, ev ? ev + 3 : nullptr,
+                     c->emit_dbg);
         if (c->emit_dbg & 0xFFFFu) {   // (development: k_emit's timing exits leave invalid streams; stop here)
             if (ev)
                 for (int q = 5; q <= kNumStages; q++) HIP_TRY(hipEventRecord(ev[q], sg));
             continue;
         }
         launch_entropy(Lg, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3], c->thist + t0 * 256,
-                       c->bhist + b0 * kStreams * 256, c->tile_off + 3 * t0, c->ctab + b0 * kStreams * 256,
+                       c->ctab + b0 * kStreams * 256,
                        c->ltab + b0 * kStreams * 256, c->hhdr + b0 * kStreams * kHuffHdrStride,
-                       c->cstat + 2 * b0 * L.cpb_total, c->blk_off + b0, total, d_out, cap, err, sg, ev ? ev + 5 : nullptr,
+                       c->cstat + 2 * b0 * L.cpb_total, c->blk_off + b0, total, d_out, cap, err, gin, c->sdesc + b0 * ((c->B + kCharSeg - 1) / kCharSeg), sg,
+                       ev ? ev + 5 : nullptr,
                        G > 1 && g > 0 ? c->gsync[3 + g - 1] : nullptr, G > 1 ? c->gsync[3 + g] : nullptr, c->emit_dbg >> 16);
     }
     if (G > 1) {

@@ -53,6 +53,7 @@ constexpr uint32_t kEncT = 128;
 constexpr uint32_t kSymL = kChunk / kEncT;   // 64
 constexpr uint32_t kSymW = kSymL / 4;        // 16 words
 static_assert(kSymL % 16 == 0, "whole 16-B loads");
+static_assert(kSymL == kCharSeg, "one chars segment descriptor per lane");
 
 __device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32_t i1, uint32_t *out32 /*kSymW words*/) {
     // loads the (up to) kSymL symbols [i0, i1) as 16-B loads, all in flight together (i0 is
@@ -82,6 +83,27 @@ __device__ inline uint32_t chunk_symbols(const uint32_t *w4, uint32_t i0, uint32
     return n;
 }
 
+// the same symbols where the lane's chars segment is a run of input bytes (k_emit's descriptor):
+// bytes p[i0, i1) at any alignment.  A whole segment is four unaligned 16-B loads (gfx950 global
+// loads take any byte address; the compiler emits the same for a byte-aligned copy); a short one
+// (the stream's last) reads its bytes one by one, so nothing past p[i1 - 1] is touched
+__device__ inline uint32_t input_symbols(const uint8_t *p, uint32_t i0, uint32_t i1, uint32_t *out32 /*kSymW words*/) {
+    const uint32_t n = i1 > i0 ? i1 - i0 : 0;
+    if (n == kSymL) {
+#pragma unroll
+        for (uint32_t q = 0; q < kSymW / 4; q++) {
+            uint4 v;
+            __builtin_memcpy(&v, p + i0 + 16 * q, 16);
+            out32[4 * q] = v.x; out32[4 * q + 1] = v.y; out32[4 * q + 2] = v.z; out32[4 * q + 3] = v.w;
+        }
+        return n;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kSymW; q++) out32[q] = 0;
+    for (uint32_t j = 0; j < n; j++) out32[j >> 2] |= (uint32_t)p[i0 + j] << (8 * (j & 3));
+    return n;
+}
+
 __device__ inline const uint8_t *stream_base(const Layout &L, uint32_t s, uint32_t b, const uint8_t *s0,
                                              const uint8_t *s1, const uint8_t *s2, const uint8_t *s3) {
     return (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
@@ -94,9 +116,7 @@ constexpr uint32_t kTreeW = kTreeT / 64;
 // kDev = true carries development timing exits (fcx_debug_emit_bits bits 16..19; the compress stops
 // after this kernel while they are set); the product launches k_tree<false>
 template <bool kDev>
-__global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__restrict__ thist,
-                                                 const uint32_t *__restrict__ bhist,
-                                                 const uint32_t *__restrict__ tile_off, const uint8_t *__restrict__ s0,
+__global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__restrict__ thist, const uint8_t *__restrict__ s0,
                                                  const uint8_t *__restrict__ s2, const uint8_t *__restrict__ s3,
                                                  BlockInfo *__restrict__ binfo, uint32_t *__restrict__ ctab,
                                                  uint8_t *__restrict__ ltab, uint8_t *__restrict__ hhdr,
@@ -141,26 +161,45 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
             w[sym] = t;
         }
     } else {
-        // the block bins (bytes wholly inside one tile's bits), then the bytes that straddle a tile
-        // boundary (each counted once: at the first boundary inside it) and the stream's zero tail
-        const uint32_t *bh = bhist + ((uint64_t)b * kStreams + s) * 256;
-#pragma unroll
-        for (uint32_t u = 0; u < 256 / kTreeT; u++) w[tid + kTreeT * u] = bh[tid + kTreeT * u];
-        __syncthreads();
-        const uint32_t comp = s == 0 ? 0u : s == 2 ? 1u : 2u;
-        const uint32_t mul = s == 2 ? kPBits : 1u;
-        const uint32_t total = s == 0 ? bi.ntok : s == 2 ? kPBits * bi.nmatch : bi.gbits;
+        // flags / distances / golomb words: the stream's slen bytes, counted straight from the
+        // finished stream (the bits past the stream's last one are zero: k_stitch cleared the words
+        // k_emit ORs into, so the (11 pCnt)/8 + 1-th byte (2192) and the golomb words' tails count
+        // as the zeros the reference counts).  Zero and 0xFF bytes (runs of flags and unary golomb
+        // codes) are counted in registers, the rest by LDS atomics
         const uint8_t *sb = (s == 0 ? s0 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
-        const uint32_t *to = tile_off + 3ull * b * L.tpb;
-        for (uint32_t k = 1 + tid; k <= ntl; k += kTreeT) {
-            const uint32_t B = k < ntl ? mul * to[3 * k + comp] : total;
-            const uint32_t P = k > 1 ? mul * to[3 * (k - 1) + comp] : 0u;
-            if ((B & 7u) && !((P >> 3) == (B >> 3) && (P & 7u))) atomicAdd(&w[sb[B >> 3]], 1u);
+        const uint32_t nby = bi.slen[s], nq = nby / 16;
+        w[tid] = 0;
+        __syncthreads();
+        uint32_t c00 = 0, cff = 0;
+        auto count4 = [&](uint32_t v, uint32_t nb) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t by = (v >> (8 * q)) & 0xFFu;
+                if (q >= nb) break;
+                if (by == 0) c00++;
+                else if (by == 0xFFu) cff++;
+                else atomicAdd(&w[by], 1u);
+            }
+        };
+        const uint4 *s4 = (const uint4 *)sb;   // (stream strides are multiples of 16)
+        constexpr uint32_t kDeep = 8;          // 16-B loads in flight per lane (text distances: ~200 KB a block)
+        for (uint32_t q0 = 0; q0 < nq; q0 += kDeep * kTreeT) {
+            uint4 v[kDeep];
+#pragma unroll
+            for (uint32_t u = 0; u < kDeep; u++) {
+                const uint32_t q = q0 + tid + kTreeT * u;
+                v[u] = q < nq ? s4[q] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kDeep; u++) {
+                const uint32_t nb = q0 + tid + kTreeT * u < nq ? 4u : 0u;
+                count4(v[u].x, nb); count4(v[u].y, nb); count4(v[u].z, nb); count4(v[u].w, nb);
+            }
         }
-        if (tid == 0) {
-            if (s == 2 && (total & 7u) == 0) atomicAdd(&w[0], 1u);   // the (11 pCnt)/8 + 1-th byte (2192)
-            if (s == 3) atomicAdd(&w[0], 4 * ((total + 31) / 32) - (total + 7) / 8);   // zero bytes up to the word end
-        }
+        if (tid < nby - 16 * nq) count4(sb[16 * nq + tid], 1);
+        c00 = wave_sum_u32(c00);
+        cff = wave_sum_u32(cff);
+        if (lane == 0) { atomicAdd(&w[0], c00); atomicAdd(&w[0xFF], cff); }
         __syncthreads();
     }
     if (dbg & 1u) { if (w[tid] == 0x12345u) err[1] = 1; return; }   // (timing: weights only)
@@ -378,7 +417,8 @@ __global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void
                                                  const uint32_t *__restrict__ ctab, const uint8_t *__restrict__ ltab,
                                                  uint64_t *__restrict__ cstat,
                                                  const uint64_t *__restrict__ blk_off, uint8_t *__restrict__ out,
-                                                 const uint32_t *__restrict__ err) {
+                                                 const uint32_t *__restrict__ err, const uint8_t *__restrict__ in,
+                                                 const uint32_t *__restrict__ sdesc) {
     constexpr uint32_t kW = kEncT / 64;
     __shared__ uint32_t ct[256], lt[256];
     __shared__ uint32_t ws[kEncWords];
@@ -391,6 +431,8 @@ __global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void
     // loads in two rounds: error word + block info, then everything else at once
     const uint32_t errv = *err;
     const BlockInfo &bi = binfo[b];
+    // chars: is this lane's segment a run of input bytes (k_emit's descriptor)?
+    const uint32_t cd = s == 1 ? sdesc[(uint64_t)b * ((L.B + kCharSeg - 1) / kCharSeg) + c * (kChunk / kCharSeg) + tid] : kCdMixed;
     const uint32_t len = bi.slen[s], c0 = c * kChunk;
     if (errv || !stream_active(bi, s) || c0 >= len) return;
     const uint32_t c1 = min(len, c0 + kChunk);
@@ -402,7 +444,8 @@ __global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void
     const uint8_t *base = (s == 0 ? s0 : s == 1 ? s1 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
     const uint32_t i0 = c0 + kSymL * tid, i1 = min(c1, i0 + kSymL);
     uint32_t sym[kSymW];
-    const uint32_t n = chunk_symbols((const uint32_t *)base, i0, i1, sym);
+    const uint32_t n = cd != kCdMixed ? input_symbols(in + (uint64_t)b * L.B + cd, i0, i1, sym)
+                                      : chunk_symbols((const uint32_t *)base, i0, i1, sym);
     const uint32_t n_chunk = c1 - c0;
     const uint64_t obyte = blk_off[b] + bi.words_rel[s];
     uint64_t *st = cstat + 2 * ((uint64_t)b * L.cpb_total + r);   // this chunk's words; st[-2k]: k chunks back
@@ -604,21 +647,21 @@ __global__ __launch_bounds__(64) void k_headers(const BlockInfo *__restrict__ bi
 
 // ---------------------------------------------------------------------------
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
-                    const uint16_t *thist, const uint32_t *bhist, const uint32_t *tile_off, uint32_t *ctab,
+                    const uint16_t *thist, uint32_t *ctab,
                     uint8_t *ltab, uint8_t *hhdr, uint64_t *cstat, uint64_t *blk_off, uint64_t *total, uint8_t *out,
-                    uint64_t cap, uint32_t *err, hipStream_t st, hipEvent_t *ev, hipEvent_t wait_scan,
-                    hipEvent_t rec_scan, uint32_t tree_dbg) {
+                    uint64_t cap, uint32_t *err, const uint8_t *in, const uint32_t *sdesc, hipStream_t st, hipEvent_t *ev,
+                    hipEvent_t wait_scan, hipEvent_t rec_scan, uint32_t tree_dbg) {
     const uint32_t nchunks = L.nblocks * L.cpb_total;
     if (ev) (void)hipEventRecord(ev[0], st);   // (the histograms are k_emit's: no stage of their own)
     if (tree_dbg) {   // (development: k_tree's timing exits; nothing after it runs)
-        hipLaunchKernelGGL(k_tree<true>, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, bhist, tile_off, s0,
-                           s2, s3, binfo, ctab, ltab, hhdr, cstat, err, tree_dbg);
+        hipLaunchKernelGGL(k_tree<true>, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, s0, s2, s3, binfo,
+                           ctab, ltab, hhdr, cstat, err, tree_dbg);
         if (ev)
             for (int q = 1; q <= 6; q++) (void)hipEventRecord(ev[q], st);
         return;
     }
-    hipLaunchKernelGGL(k_tree<false>, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, bhist, tile_off, s0, s2,
-                       s3, binfo, ctab, ltab, hhdr, cstat, err, 0u);
+    hipLaunchKernelGGL(k_tree<false>, dim3(L.nblocks * kStreams), dim3(kTreeT), 0, st, L, thist, s0, s2, s3, binfo, ctab,
+                       ltab, hhdr, cstat, err, 0u);
     if (ev) (void)hipEventRecord(ev[1], st);
     hipLaunchKernelGGL(k_block_layout, dim3((L.nblocks + 63) / 64), dim3(64), 0, st, L.nblocks, binfo);
     if (ev) (void)hipEventRecord(ev[2], st);
@@ -628,7 +671,7 @@ void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1,
     if (ev) (void)hipEventRecord(ev[3], st);
     if (ev) (void)hipEventRecord(ev[4], st);   // (no edge zeroing: k_encode stores every word whole)
     hipLaunchKernelGGL(k_encode, dim3(nchunks), dim3(kEncT), 0, st, L, binfo, s0, s1, s2, s3, ctab, ltab, cstat,
-                       blk_off, out, err);
+                       blk_off, out, err, in, sdesc);
     if (ev) (void)hipEventRecord(ev[5], st);
     hipLaunchKernelGGL(k_headers, dim3(L.nblocks), dim3(64), 0, st, binfo, s0, L.sstride[0], hhdr, blk_off, out, err);
     if (ev) (void)hipEventRecord(ev[6], st);

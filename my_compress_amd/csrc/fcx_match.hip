@@ -39,6 +39,10 @@
 
 #include "fcx_device.h"
 
+#ifndef FCX_MATCH_EXIT
+#define FCX_MATCH_EXIT 0u   // development: a dbg timing-exit bit compiled into the product kernel (tools/phase_libs.sh)
+#endif
+
 namespace fcx {
 
 constexpr uint32_t kWinPos = kHalo + 1 + kTile;      // 6144 window positions per tile
@@ -724,7 +728,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
                                               uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg_in) {
-    const uint32_t dbg = kDev ? dbg_in : 0u;
+    const uint32_t dbg = kDev ? dbg_in : (uint32_t)FCX_MATCH_EXIT;   // (FCX_MATCH_EXIT: phase-timing builds only)
     __shared__ __attribute__((aligned(16))) uint32_t sdw[kTileBytes / 4 + 4];   // byte image of the window
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
     // search, [step (u16 x 4096) | parse scratch] after it

@@ -353,7 +353,7 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                                                const uint32_t *__restrict__ mtok, uint32_t *__restrict__ tile_off,
                                                uint32_t *__restrict__ tconv, BlockInfo *__restrict__ binfo,
                                                uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_p,
-                                               uint8_t *__restrict__ s_golomb, uint32_t *__restrict__ bhist) {
+                                               uint8_t *__restrict__ s_golomb) {
     __shared__ uint32_t mL[kTile];
     __shared__ uint32_t sti[64][6];          // per tile of the batch: flags, exit, totals, k_resolve verdict
     __shared__ uint32_t sfp[64][5];          // k_resolve: final counts, exit, conv record
@@ -370,7 +370,6 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
     const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
     const uint8_t *d = in + bstart;
     const uint32_t ntiles = (blen + kTile - 1) / kTile;
-    for (uint32_t x = lane; x < kStreams * 256; x += 64) bhist[(uint64_t)b * kStreams * 256 + x] = 0;   // k_emit's bins
     uint32_t e = 0, dbase = 0xFFFFFFFFu, nlazy = 0, lazy_tiles = 0;
     Cnt3 run{0, 0, 0};
     uint4 pv[kTile / 256];   // prefetched rows / mbits / chain word of tile pk
@@ -706,12 +705,26 @@ __device__ inline void flush_words(uint32_t *g, uint32_t gw0, const uint32_t *w,
     }
 }
 
-// all-literal tile (random data): the tile's chars are its input bytes (staged in LDS),
-// its flags all ones; output dwords on the stream's dword grid by alignbyte, the
-// partial dwords at the tile's two ends as byte stores
-__device__ void emit_literal_tile(const uint32_t *lin, uint32_t nt, uint32_t tok0, uint8_t *chars, uint32_t *flags) {
+// all-literal tile (random data): the tile's chars are its input bytes (staged in LDS), its flags
+// all ones.  k_encode reads the chars of the segments that lie wholly inside the tile [sa, sz) straight
+// from the input (their descriptors say so), so only the chars outside them go to the stream: the
+// head and tail partial segments as byte stores.  (sa >= sz: every char, as dwords on the stream's
+// dword grid by alignbyte, the partial dwords at the two ends as byte stores.)
+__device__ void emit_literal_tile(const uint32_t *lin, uint32_t nt, uint32_t tok0, uint32_t sa, uint32_t sz, uint8_t *chars,
+                                  uint32_t *flags) {
     const uint32_t tid = threadIdx.x;
+    const uint32_t f0 = tok0, f1 = tok0 + nt;
+    for (uint32_t w = (f0 >> 5) + tid; w <= ((f1 - 1) >> 5); w += 256) {
+        const uint32_t lo = max(f0, 32 * w), hi = min(f1, 32 * w + 32);
+        if (hi - lo == 32) flags[w] = ~0u;
+        else atomicOr(&flags[w], ((1u << (hi - lo)) - 1u) << (lo - 32 * w));
+    }
     const uint8_t *lb = (const uint8_t *)lin;
+    if (sa < sz) {
+        if (tid < sa - tok0) chars[tok0 + tid] = lb[tid];
+        if (tid < f1 - sz) chars[sz + tid] = lb[sz - tok0 + tid];
+        return;
+    }
     const uint32_t e = (4u - (tok0 & 3u)) & 3u;             // input byte of the first whole output dword
     const uint32_t nfull = nt >= e ? (nt - e) >> 2 : 0u;      // whole output dwords
     uint32_t *c4 = (uint32_t *)chars + ((tok0 + e) >> 2);
@@ -723,41 +736,16 @@ __device__ void emit_literal_tile(const uint32_t *lin, uint32_t nt, uint32_t tok
     const uint32_t zf = e + 4 * nfull;
     if (tid < min(e, nt)) chars[tok0 + tid] = lb[tid];
     if (tid < nt - min(zf, nt)) chars[tok0 + zf + tid] = lb[zf + tid];
-    const uint32_t f0 = tok0, f1 = tok0 + nt;
-    for (uint32_t w = (f0 >> 5) + tid; w <= ((f1 - 1) >> 5); w += 256) {
-        const uint32_t lo = max(f0, 32 * w), hi = min(f1, 32 * w + 32);
-        if (hi - lo == 32) flags[w] = ~0u;
-        else atomicOr(&flags[w], ((1u << (hi - lo)) - 1u) << (lo - 32 * w));
-    }
 }
 
-// ---- symbol histograms of the block's four Huffman sub-streams, built here while each tile's
-// stream bits are still in LDS (my_huffman_encode_char's count, my_compress.cpp:998-1000):
-// the tile counts its chars (one byte per token) and the flag / distance / golomb bytes that lie
-// wholly inside its bits; a byte that straddles two tiles' bits (or the stream's zero tail) is
-// k_tree's, read back from the finished stream.  Chars go out as the tile's row of u16 counts
-// (one plain 512-B store), the other three streams by atomics into the block's bins (few bins
-// per tile on random data).
-__device__ inline void hist_inside(const uint32_t *w, uint64_t b0, uint64_t b1, uint32_t *h, uint32_t tid) {
-    const uint64_t wbase = b0 >> 5;   // staged word 0 = global word b0 >> 5
-    const uint64_t k0 = (b0 + 7) >> 3, k1 = b1 >> 3;
-    for (uint64_t k = k0 + tid; k < k1; k += 256)
-        atomicAdd(&h[(w[(k >> 2) - wbase] >> (8 * (k & 3))) & 0xFFu], 1u);
-}
+// ---- the chars histogram (my_huffman_encode_char's count, my_compress.cpp:998-1000), built here
+// while the tile's chars are in LDS or registers: one row of u16 counts per tile (one plain 512-B
+// store), summed by k_tree.  The flag / distance / golomb streams are short (text: 0.33 MB per
+// MiB) and k_tree counts their bytes straight from the finished streams.
 __device__ inline void hist_bytes16(const uint32_t in4[4], uint32_t n, uint32_t *h) {   // the first n of 16 bytes
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++)
         if (q < n) atomicAdd(&h[(in4[q >> 2] >> (8 * (q & 3))) & 0xFFu], 1u);
-}
-// after a barrier: the tile's chars row and the block bins of the other streams
-__device__ inline void hist_flush(const uint32_t (*hh)[256], uint16_t *trow, uint32_t *bh, uint32_t tid) {
-    trow[tid] = (uint16_t)hh[1][tid];
-#pragma unroll
-    for (uint32_t q = 0; q < 3; q++) {
-        const uint32_t st = q == 0 ? 0u : q + 1;
-        const uint32_t v = hh[st][tid];
-        if (v) atomicAdd(&bh[st * 256 + tid], v);
-    }
 }
 
 constexpr uint32_t kInW = (kTile + kLookAhead) / 4 + 2;   // tile input + look-ahead (dwords)
@@ -775,10 +763,10 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
                                               const uint32_t *__restrict__ tconv, const uint32_t *__restrict__ tinfo,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb,
-                                              uint16_t *__restrict__ thist, uint32_t *__restrict__ bhist, uint32_t dbg_in) {
+                                              uint16_t *__restrict__ thist, uint32_t *__restrict__ sdesc, uint32_t dbg_in) {
     const uint32_t dbg = kDev ? dbg_in : 0u;
     __shared__ uint32_t sh[16];
-    __shared__ uint32_t hh[kStreams][256];   // this tile's symbol counts per stream
+    __shared__ uint32_t hc[256];             // this tile's chars counts
     __shared__ uint32_t lf[kFlagW], lp[kPW], lg[kGW], lc[kCharW];
     __shared__ uint32_t lin[kInW];           // input bytes [t0, t0 + kTile + kLookAhead) of the block
     __shared__ uint32_t lmt[kTileMatches];   // the tile's compact match list from its conv point
@@ -790,9 +778,8 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     if (t0 >= blen) return;
     const uint32_t t1 = min(blen, t0 + kTile);
     const uint32_t tix = blockIdx.x;
-    for (uint32_t x = tid; x < kStreams * 256; x += 256) (&hh[0][0])[x] = 0;   // (every path's barriers order it)
+    hc[tid] = 0;   // (every path's barriers order it)
     uint16_t *trow = thist + (uint64_t)tix * 256;
-    uint32_t *bh = bhist + (uint64_t)b * kStreams * 256;
 
     // ---- round 1: independent loads ----
     const bool last = t1 == blen;
@@ -823,6 +810,15 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
                 if (s + 4 * q + j < blen) w |= (uint32_t)d[s + 4 * q + j] << (8 * j);
             in4[q] = w;
         }
+    }
+    // descriptors of the chars segments (kCharSeg chars: one k_encode lane's symbols) that start in this
+    // tile: a segment wholly inside an all-literal tile (as many tokens as positions, no match; the
+    // block's last segment may end past the stream) is the input bytes from char + t0 - tok0
+    const bool lit = tk1 - tok0 == t1 - t0 && mk1 == mi0;
+    const uint32_t sa = (tok0 + kCharSeg - 1) / kCharSeg * kCharSeg, sz = last ? tk1 : tk1 / kCharSeg * kCharSeg;   // inside: [sa, sz)
+    if (tid < (tk1 + kCharSeg - 1) / kCharSeg - sa / kCharSeg) {
+        const uint32_t g = sa / kCharSeg + tid;
+        sdesc[(uint64_t)b * ((L.B + kCharSeg - 1) / kCharSeg) + g] = lit && kCharSeg * g < sz ? t0 - tok0 : kCdMixed;
     }
     uint32_t la = 0;   // look-ahead dword (match chars past the tile end)
     const uint32_t xa = t0 + kTile + 4 * tid;
@@ -884,31 +880,22 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         flush_words((uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]), fw0, lf, nfw, tid);
         flush_words((uint32_t *)(s_p + (uint64_t)b * L.sstride[2]), pw0, lp, npw, tid);
         flush_words((uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]), gw0, lg, ngw, tid);
-        if (tid == 0 && tot[0]) hh[1][ub] += tot[0];   // every token's char is the tile's byte
-        hist_inside(lf, tok0, tok0 + tot[0], hh[0], tid);
-        hist_inside(lp, (uint64_t)kPBits * mi0, (uint64_t)kPBits * (mi0 + tot[1]), hh[2], tid);
-        hist_inside(lg, g0, (uint64_t)g0 + tot[2], hh[3], tid);
-        __syncthreads();
-        hist_flush(hh, trow, bh, tid);
+        trow[tid] = tid == ub ? (uint16_t)tot[0] : (uint16_t)0;   // every token's char is the tile's byte
         return;
     }
 #pragma unroll
     for (uint32_t q = 0; q < 4; q++) lin[4 * tid + q] = in4[q];
     if (tid < kInW - kTile / 4) lin[kTile / 4 + tid] = la;
 
-    if (tk1 - tok0 == t1 - t0 && mk1 == mi0) {   // no match token in the tile (uniform)
+    if (lit) {   // no match token in the tile
         if (dbg & 1u) { if (s < t1 && (in4[0] ^ (uint32_t)cwv) == 0x12345u) trow[tid] = 1; return; }   // (timing)
         __syncthreads();
-        emit_literal_tile(lin, t1 - t0, tok0, s_chars + (uint64_t)b * L.sstride[1],
+        emit_literal_tile(lin, t1 - t0, tok0, sa, sz, s_chars + (uint64_t)b * L.sstride[1],
                           (uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]));
         // chars = the tile's bytes; every whole flag byte is 0xFF
-        hist_bytes16(in4, s < t1 ? min(16u, t1 - s) : 0u, hh[1]);
-        if (tid == 0) {
-            const uint32_t k0 = (tok0 + 7) >> 3, k1 = (tok0 + (t1 - t0)) >> 3;
-            if (k1 > k0) hh[0][0xFF] += k1 - k0;
-        }
+        hist_bytes16(in4, s < t1 ? min(16u, t1 - s) : 0u, hc);
         __syncthreads();
-        hist_flush(hh, trow, bh, tid);
+        trow[tid] = (uint16_t)hc[tid];
         return;
     }
 
@@ -1004,7 +991,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         }
         fl = 0xFFFFu;
         nt_lane = 16;
-        hist_bytes16(in4, 16, hh[1]);
+        hist_bytes16(in4, 16, hc);
     } else
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
@@ -1012,7 +999,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
             const uint32_t Lm = m_len(mm[q]);
             const uint8_t ch = Lm ? lb[s - t0 + q + Lm] : (uint8_t)(in4[q >> 2] >> (8 * (q & 3)));
             lcb[tokA + nt_lane - 4 * cw0] = ch;
-            atomicAdd(&hh[1][ch], 1u);
+            atomicAdd(&hc[ch], 1u);
             if (Lm == 0) {
                 fl |= 1u << nt_lane;
             } else {
@@ -1058,30 +1045,26 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     flush_words((uint32_t *)(s_flags + (uint64_t)b * L.sstride[0]), fw0, lf, nfw, tid);
     flush_words((uint32_t *)(s_p + (uint64_t)b * L.sstride[2]), pw0, lp, npw, tid);
     flush_words((uint32_t *)(s_golomb + (uint64_t)b * L.sstride[3]), gw0, lg, ngw, tid);
-    hist_inside(lf, tok0, tok0 + tot[0], hh[0], tid);
-    hist_inside(lp, (uint64_t)kPBits * mi0, (uint64_t)kPBits * (mi0 + tot[1]), hh[2], tid);
-    hist_inside(lg, g0, (uint64_t)g0 + tot[2], hh[3], tid);
-    __syncthreads();
-    hist_flush(hh, trow, bh, tid);
+    trow[tid] = (uint16_t)hc[tid];   // (the barrier after the token loop ordered the counts)
 }
 
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *bhist, hipStream_t st, hipEvent_t *ev,
-                  uint32_t emit_dbg) {
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *sdesc, hipStream_t st,
+                  hipEvent_t *ev, uint32_t emit_dbg) {
     const uint32_t ntiles = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_resolve, dim3(ntiles), dim3(64), 0, st, L, m, mbits, chain, chain_pfx, tinfo, fp);
     hipLaunchKernelGGL(k_stitch, dim3(L.nblocks), dim3(64), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, fp, mtok,
-                       tile_off, tconv, binfo, s_flags, s_p, s_golomb, bhist);
+                       tile_off, tconv, binfo, s_flags, s_p, s_golomb);
     if (ev) (void)hipEventRecord(ev[0], st);
     emit_dbg &= 0xFFFFu;   // (bits 16.. are k_tree's)
     if (emit_dbg == 0)
         hipLaunchKernelGGL(k_emit<false>, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok,
-                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, bhist, 0u);
+                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, sdesc, 0u);
     else
         hipLaunchKernelGGL(k_emit<true>, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok,
-                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, bhist, emit_dbg);
+                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, sdesc, emit_dbg);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 

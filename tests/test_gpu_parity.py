@@ -186,6 +186,36 @@ def test_dense_and_periodic_edges(gpu_compress):
             assert gpu_compress(data, block) == oracle.compress_file(data, block), (len(data), block)
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3, 6, 13])
+def test_literal_tiles_read_from_input(cuda, shift):
+    """all-literal tiles keep their chars in the input: k_emit marks the 64-char segments wholly
+    inside them and k_encode reads those from the input at whatever alignment they have.  Random
+    data with short repeats planted every few tiles puts literal tiles next to matching ones at
+    every chars alignment; the device input starts at every alignment too"""
+    import torch
+
+    rng = random.Random(99 + shift)
+    data = bytearray(inputs.generate("rand", 11, 3 << 20))
+    for _ in range(300):
+        src = rng.randrange(len(data) - 4096)
+        dst, ln = src + rng.randrange(5, 2000), rng.randrange(3, 40)
+        data[dst:dst + ln] = data[src:src + ln]
+    data = bytes(data)
+    buf = torch.zeros(len(data) + 16, dtype=torch.uint8, device=cuda)
+    buf[shift:shift + len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
+    for block in (1 << 20, 65536, 10000):
+        ctx = mc.Context(0, block, len(data))
+        try:
+            cap = mc.shard_bound(len(data), block)
+            d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+            n = ctx.compress_shard(buf.data_ptr() + shift, len(data), d_out.data_ptr(), cap,
+                                   torch.cuda.current_stream().cuda_stream)
+            got = mc.write_header(len(data), (len(data) + block - 1) // block) + d_out[:n].cpu().numpy().tobytes()
+            assert got == oracle.compress_file(data, block), (shift, block)
+        finally:
+            ctx.close()
+
+
 @pytest.mark.parametrize("block", [1 << 20, 65536])
 def test_dna_vs_oracle(gpu_compress, block):
     """'ACGT'[rand()%4]: 64 distinct 3-byte keys, ~32 same-key candidates per
