@@ -232,7 +232,22 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
     __syncthreads();
     if (dbg & 2u) { if (sw[tid] == 0x12345u) err[1] = 1; return; }   // (timing: + rank sort)
     const uint32_t nint = real >= 2 ? real - 1 : 0;
-    if (tid == 0 && nint) {
+    // When the two lightest leaves outweigh the heaviest (w0 + w1 > w_max: the chars of random data),
+    // every internal node outweighs every leaf, so the leaves are consumed first, in pairs, and the
+    // sequence S = sorted leaves, then internal nodes in creation order, is nondecreasing (node k =
+    // S[2k] + S[2k+1] >= S[2k-2] + S[2k-1] = node k-1): the merge takes S[2k] (left) and S[2k+1]
+    // (right) at step k, a closed form every thread evaluates for its own nodes
+    const bool fifo = nint && sw[0] + sw[1] > sw[real - 1];
+    if (fifo) {
+        for (uint32_t kk = tid; kk < nint; kk += kTreeT) {
+            const uint32_t a = 2 * kk, c = 2 * kk + 1;
+            const uint32_t id0 = a < real ? ss[a] : 256 + (a - real), id1 = c < real ? ss[c] : 256 + (c - real);
+            il[kk] = id0;
+            ir[kk] = id1;
+            par[id0] = 256 + kk;
+            par[id1] = 256 + kk;
+        }
+    } else if (tid == 0 && nint) {
         // two-queue merge == the reference's sorted-list re-insertion (570-611).  Each step
         // reads both queue heads two deep at once (one LDS round trip per step)
         uint32_t lq = 0, iq = 0;

@@ -20,4 +20,4 @@ PY
 rm -f fm_v_$name*
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/libfcx_$name.so build/v_$name/$tgt.o $(ls build/*.o | grep -v $tgt.o) \
     -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-rm -rf build/v_$name
+rm -rf build/v_$name ../lib/libfcx.so.[0-9]*
