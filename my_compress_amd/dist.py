@@ -58,8 +58,8 @@ def piece_ranges(n: int, block_bytes: int, nsub: int):
 
 # ---- the strong-scaling step model --------------------------------------------
 # One GPU's compress time per GiB and output ratio for each synthetic kind at 1 MiB blocks
-# (bench.py on one MI355X, profiles/r03_bench_n1.json), the defaults of gather_share_ppm.
-COMPRESS_MS_PER_GIB = {"rand": 4.8, "text": 14.1, "zeros": 3.4, "runs": 12.0, "dna": 57.7}
+# (bench.py on one MI355X, profiles/r04_bench_n1.json), the defaults of gather_share_ppm.
+COMPRESS_MS_PER_GIB = {"rand": 4.54, "text": 14.06, "zeros": 3.33, "runs": 11.92, "dna": 57.85}
 RATIO = {"rand": 1.0164, "text": 0.582, "zeros": 0.007, "runs": 0.0396, "dna": 0.27}
 
 
