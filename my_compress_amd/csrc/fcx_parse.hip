@@ -230,19 +230,23 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     // prefetch: chain + mbits words below the span (lanes 0..nw-1), m of those positions
     uint64_t wv = 0, mv = 0;
     if (lane < nw) { wv = cw[lane]; mv = mb[lane]; }
-    uint32_t mreg[kResW];
-#pragma unroll
-    for (uint32_t q = 0; q < kResW; q++) {
-        const uint32_t x = 64 * q + lane;
-        const uint64_t mbq = __shfl(mv, q, 64);
-        mreg[q] = (q < nw && x < t1 - t0 && ((mbq >> lane) & 1ull)) ? (uni ? m_uniform(t0 + x, blen) : mt[x]) : 0u;
-    }
     // chain / mbits words stay distributed (lane q holds word q); the walk reads word q of the
     // wave-uniform position by readlane, and lane q keeps the walked bits of word q
     auto word_at = [](uint64_t v, uint32_t q) -> uint64_t {
         return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)q) |
                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)q) << 32);
     };
+    // the assumed entry on the speculative chain (the previous tile's exit is t0 and the chain
+    // starts there: random data's tiles): the walk ends before it starts, no m row is needed
+    const bool at_chain = rel0 < t1 - t0 && ((word_at(wv, fcx::uni(rel0 >> 6)) >> (rel0 & 63)) & 1ull);
+    uint32_t mreg[kResW];
+#pragma unroll
+    for (uint32_t q = 0; q < kResW; q++) {
+        const uint32_t x = 64 * q + lane;
+        const uint64_t mbq = __shfl(mv, q, 64);
+        mreg[q] = (!at_chain && q < nw && x < t1 - t0 && ((mbq >> lane) & 1ull)) ? (uni ? m_uniform(t0 + x, blen) : mt[x])
+                                                                                : 0u;
+    }
     uint64_t nwb = 0;
     // walk from the assumed entry until it meets the speculative chain (uniform over the wave)
     Cnt3 walked{0, 0, 0};
