@@ -112,6 +112,8 @@ __device__ inline const uint8_t *stream_base(const Layout &L, uint32_t s, uint32
 // ---------------------------------------------------------------------------
 constexpr uint32_t kTreeT = 256;   // k_tree workgroup: four waves (the chars rows are summed by all of them; the merge is serial)
 constexpr uint32_t kTreeW = kTreeT / 64;
+constexpr uint32_t kJacobiMin = 64, kJacobiMax = 40;   // k_tree: merges solved as a fixed point
+static_assert(kTreeW * 256 >= 2 * 512, "the fixed point's P arrays in the weights scratch");
 
 // kDev = true carries development timing exits (fcx_debug_emit_bits bits 16..19; the compress stops
 // after this kernel while they are set); the product launches k_tree<false>
@@ -247,7 +249,55 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
             par[id0] = 256 + kk;
             par[id1] = 256 + kk;
         }
-    } else if (tid == 0 && nint) {
+    }
+    // Otherwise a long merge (>= kJacobiMin internal nodes) is solved as a fixed point, all threads
+    // at once: the picks P are the sorted merge of the leaves L and the internal weights I (a leaf
+    // first on a tie) and I[k] = P[2k] + P[2k+1].  From I = infinity, each round ranks every leaf and
+    // internal node into P by binary search and recomputes I; I only decreases towards the merge's
+    // (I[0] is right after one round, and I[k] is right one round after every node P[0..2k+1] uses),
+    // and the measured histograms settle in 8-15 rounds.  Past kJacobiMax rounds, or for short
+    // merges, one thread runs the two-queue merge below.
+    bool merged = fifo;
+    if (!fifo && nint >= kJacobiMin) {
+        constexpr uint32_t kInf = 0xFFFFFFFFu;
+        uint32_t *pw = &part[0][0], *pid = &part[2][0];   // P's weights and ids (the weights phase is over)
+        for (uint32_t kk = tid; kk < nint; kk += kTreeT) iw[kk] = kInf;
+        __syncthreads();
+        for (uint32_t it = 0; it < kJacobiMax && !merged; it++) {
+            for (uint32_t t = tid; t < real; t += kTreeT) {   // leaf t: after the internal nodes lighter than it
+                const uint32_t wl = sw[t];
+                uint32_t lo = 0, hi = nint;
+                while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (iw[md] < wl) lo = md + 1; else hi = md; }
+                pw[t + lo] = wl;
+                pid[t + lo] = ss[t];
+            }
+            for (uint32_t j = tid; j < nint; j += kTreeT) {   // internal j: after the leaves no heavier than it
+                const uint32_t wi = iw[j];
+                uint32_t lo = 0, hi = real;
+                while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (sw[md] <= wi) lo = md + 1; else hi = md; }
+                pw[j + lo] = wi;
+                pid[j + lo] = 256 + j;
+            }
+            __syncthreads();
+            bool ch = false;
+            for (uint32_t kk = tid; kk < nint; kk += kTreeT) {
+                const uint32_t a = pw[2 * kk], c = pw[2 * kk + 1];
+                const uint32_t nv = (a == kInf || c == kInf) ? kInf : a + c;
+                ch = ch || nv != iw[kk];
+                iw[kk] = nv;   // (read by the other threads only after the barrier below)
+            }
+            merged = __syncthreads_or(ch ? 1 : 0) == 0;
+        }
+        if (merged)
+            for (uint32_t kk = tid; kk < nint; kk += kTreeT) {
+                const uint32_t id0 = pid[2 * kk], id1 = pid[2 * kk + 1];
+                il[kk] = id0;
+                ir[kk] = id1;
+                par[id0] = 256 + kk;
+                par[id1] = 256 + kk;
+            }
+    }
+    if (!merged && tid == 0 && nint) {
         // two-queue merge == the reference's sorted-list re-insertion (570-611).  Each step
         // reads both queue heads two deep at once (one LDS round trip per step)
         uint32_t lq = 0, iq = 0;
