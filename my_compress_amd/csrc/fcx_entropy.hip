@@ -13,14 +13,16 @@
 // per (block, stream), then serialises the tree (1013-1066) and the code table:
 // code = root->leaf path, left = 0, root decision in bit 0 (LSB-first, 869-924).
 //
-//   (histograms)   built by k_emit while each tile's stream bits are in LDS (fcx_parse.hip):
-//                  a u16 row of chars counts per tile, block bins for the other streams
-//   k_tree         sums a stream's counts (plus the bytes that straddle two tiles' bits and
-//                  the stream's zero tail, read back here), builds the tree, header bytes,
-//                  code table and W, and clears the stream's chunk status words
+//   (histograms)   the chars: a u16 row of counts per tile, built by k_emit (fcx_parse.hip)
+//   k_tree         sums the chars rows, or counts the bytes of a finished flag / distance /
+//                  golomb stream; builds the tree (closed form for balanced weights, a fixed
+//                  point for other long merges, else the serial two-queue merge), header
+//                  bytes, code table and W, and clears the stream's chunk status words
 //   k_block_layout record layout and size per block
 //   k_scan_blocks  record offsets across the shard (+ capacity check)
-//   k_encode       a chunk of 8192 symbols per workgroup: its bit count, then its starting bit
+//   k_encode       a chunk of 8192 symbols per workgroup (a chars lane whose 64 symbols are a run
+//                  of input bytes, per k_emit's segment descriptor, reads them from the input):
+//                  its bit count, then its starting bit
 //                  by decoupled look-back over the stream's earlier chunks (8-byte status
 //                  words: aggregate or inclusive prefix, and the chunk's last 32 code bits);
 //                  each lane packs its 64 codes into whole words in LDS; the words are stored

@@ -22,7 +22,10 @@
 //             2073-2113, the split at 2150-2161, combine_bits 1292-1313,
 //             golomb_rice_encode 258-304): bits are gathered per lane, merged in
 //             LDS and stored as whole words (edge words of a tile by atomicOr);
-//             chars are staged in LDS and stored as aligned dwords.
+//             chars are staged in LDS and stored as aligned dwords, except those of
+//             all-literal tiles, which stay in the input: a descriptor per 64 chars
+//             tells k_encode where to read them.  The tile's chars histogram goes out
+//             as a row of u16 counts.
 #include "fcx_device.h"
 
 namespace fcx {
