@@ -651,7 +651,18 @@ def main():
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(mc.dist_unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, src=0)
-        args.fcx_dist = mc.Dist.rank(world, rank, bytes(uid.cpu().numpy().tobytes()), dev.index)
+        try:
+            args.fcx_dist = mc.Dist.rank(world, rank, bytes(uid.cpu().numpy().tobytes()), dev.index)
+            ok = 1
+        except mc.FcxError as e:   # (the line then says concat_impl "torch.distributed (nccl)")
+            print(f"rank {rank}: fcx_dist_init_rank failed ({e}); the torch.distributed path carries the exchange",
+                  file=sys.stderr, flush=True)
+            args.fcx_dist, ok = None, 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)   # every rank takes the same path
+        if not int(flag.item()) and args.fcx_dist is not None:
+            args.fcx_dist.close()
+            args.fcx_dist = None
     main_res = run_leg(args.kind, SEEDS[args.kind], args.block, args, rank, world, dev, dist, True,
                        scaling=args.scaling, main_leg=True)
     legs = {}
