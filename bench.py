@@ -116,6 +116,90 @@ def timed(fn, steps, dist, dev):
     return max_over_ranks(time.perf_counter() - t0, dist, dev)
 
 
+def setup_leg(kind, seed, block, args, rank, world, dev, scaling, n_global, share0, concat, main_leg):
+    """this rank's input (device-resident) and output buffers for one partition of the leg"""
+    import torch
+
+    import my_compress_amd as mc
+    from my_compress_amd import dist as fdist
+
+    if scaling == "strong":
+        ranges = [fdist.byte_range(n_global, block, r, world, share0) for r in range(world)]
+    else:
+        per = n_global // world
+        ranges = [(r * per, (r + 1) * per) for r in range(world)]
+    lo, hi = ranges[rank]
+    S = {"ranges": ranges, "rank_bytes": [b - a for a, b in ranges], "n": hi - lo, "share0": share0}
+    n = S["n"]
+    t = time.time()
+    if scaling == "weak" and kind != "rand":
+        host = make_input(kind, seed + rank, 0, n)   # independent per-rank streams
+    else:
+        host = make_input(kind, seed, lo, hi)
+    S["gen_s"] = time.time() - t
+    S["d_in"] = host.to(dev)
+    S["host_path"] = None
+    if world == 1 and args.host_path and main_leg:
+        S["host_path"] = host_leg(host, n, block)
+    del host
+    # gather / pipe: rank 0's compress output buffer is also the file buffer (its segment sits at
+    # offset 0); pipe: a peer's pieces sit at their bound offsets
+    cap = mc.shard_bound(n_global if (concat in ("gather", "pipe") and rank == 0) else n, block)
+    if concat == "pipe" and rank != 0:
+        cap = mc.dist_gather_bound(n, block, args.nsub)
+    S["cap"] = cap
+    S["d_out"] = torch.empty(cap, dtype=torch.uint8, device=dev)
+    S["whole"] = None
+    if concat == "allgather":
+        S["whole"] = torch.empty(mc.shard_bound(n_global, block), dtype=torch.uint8, device=dev)
+    S["ctx"] = mc.Context(dev.index, block, max(n, block))
+    return S
+
+
+def calibrate_leg(S, kind, block, args, rank, world, dev, dist):
+    """the pipe step's partition from measurements (one warmup step): this rank's compress ms per
+    GiB (its whole shard, one timed call), its compressed bytes, and the link rate of the gather
+    pattern itself (every peer's contiguous segment to rank 0 at once, over the same transport the
+    step uses: fcx_dist_concat, or torch.distributed)"""
+    import torch
+
+    import my_compress_amd as mc
+    from my_compress_amd import dist as fdist
+
+    n, ctx, d_in, d_out, cap = S["n"], S["ctx"], S["d_in"], S["d_out"], S["cap"]
+    sid = torch.cuda.current_stream(dev).cuda_stream
+    seg = 0
+    best = float("inf")
+    for _ in range(2):   # (the first call also warms the context's scratch)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        seg = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid) if n else 0
+        best = min(best, time.perf_counter() - t0)
+    c_ms = best * 1e3 / max(n / GiB, 1e-9) if n else 0.0
+    gloo = dist.get_backend() == "gloo"
+
+    def probe():
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        if args.fcx_dist is not None:
+            args.fcx_dist.concat(d_out.data_ptr(), seg, d_out.data_ptr(), cap, mc.DIST_GATHER, sid)
+        else:
+            sizes, offs = fdist.exchange_sizes(seg, dist, "cpu" if gloo else dev)
+            if gloo:
+                buf = torch.empty(sum(sizes) + 1, dtype=torch.uint8)
+                fdist.gather_segments(d_out[:seg].cpu(), buf, sizes, offs, dist, 0)
+            else:
+                fdist.gather_segments(d_out[:seg], d_out, sizes, offs, dist, 0)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0
+
+    cal = fdist.calibrate_share(dist, kind, args.nsub, c_ms, n, seg, probe, device="cpu" if gloo else dev)
+    cal["assumed_link_gbps"] = args.link_gbps
+    cal["share0_ppm_assumed_link"] = S["share0"]
+    return cal
+
+
 def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, scaling="strong", main_leg=False,
             global_mib=None):
     """one leg.  strong: the global input of global_mib (default args.global_mib) MiB split over
@@ -129,38 +213,27 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     share0 = 0
     if scaling == "strong":
         n_global = (global_mib or args.global_mib) << 20
-        if concat == "pipe" and world > 1:   # the gather-aware partition
+        if concat == "pipe" and world > 1:   # the gather-aware partition (the model at the assumed link rate)
             share0 = args.share0_ppm if args.share0_ppm >= 0 else fdist.gather_share_ppm(
                 world, kind, args.link_gbps, args.nsub)
-        ranges = [fdist.byte_range(n_global, block, r, world, share0) for r in range(world)]
     else:
-        per = args.mib << 20
-        n_global = per * world
-        ranges = [(r * per, (r + 1) * per) for r in range(world)]
-    lo, hi = ranges[rank]
-    rank_bytes = [b - a for a, b in ranges]
-    n = hi - lo
-    t = time.time()
-    if scaling == "weak" and kind != "rand":
-        host = make_input(kind, seed + rank, 0, n)   # independent per-rank streams
-    else:
-        host = make_input(kind, seed, lo, hi)
-    gen_s = time.time() - t
-    d_in = host.to(dev)
-    host_path = None
-    if world == 1 and args.host_path and main_leg:
-        host_path = host_leg(host, n, block)
-    del host
-    # gather / pipe: rank 0's compress output buffer is also the file buffer (its segment sits at
-    # offset 0); pipe: a peer's pieces sit at their bound offsets
-    cap = mc.shard_bound(n_global if (concat in ("gather", "pipe") and rank == 0) else n, block)
-    if concat == "pipe" and rank != 0:
-        cap = mc.dist_gather_bound(n, block, args.nsub)
-    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
-    whole = None
-    if concat == "allgather":
-        whole = torch.empty(mc.shard_bound(n_global, block), dtype=torch.uint8, device=dev)
-    ctx = mc.Context(dev.index, block, max(n, block))
+        n_global = (args.mib << 20) * world
+    S = setup_leg(kind, seed, block, args, rank, world, dev, scaling, n_global, share0, concat, main_leg)
+    calib = None
+    if concat == "pipe" and scaling == "strong" and world > 1 and args.share0_ppm < 0 and args.calibrate:
+        calib = calibrate_leg(S, kind, block, args, rank, world, dev, dist)
+        if calib["share0_ppm"] != share0:   # re-partition with the measured figures
+            nb = (n_global + block - 1) // block
+            moved = fdist.block_range(nb, 0, world, calib["share0_ppm"]) != fdist.block_range(nb, 0, world, share0)
+            share0 = calib["share0_ppm"]
+            if moved:
+                S["ctx"].close()
+                S.clear()
+                torch.cuda.empty_cache()
+                S = setup_leg(kind, seed, block, args, rank, world, dev, scaling, n_global, share0, concat, main_leg)
+    ranges, rank_bytes, n = S["ranges"], S["rank_bytes"], S["n"]
+    d_in, d_out, cap, whole, ctx = S["d_in"], S["d_out"], S["cap"], S["whole"], S["ctx"]
+    gen_s, host_path = S["gen_s"], S["host_path"]
     sid = torch.cuda.current_stream(dev).cuda_stream
     state = {}
 
@@ -194,7 +267,8 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
                     tot = fdist.compress_gather(None, dist, rank_bytes, block, args.nsub, own=own, out=d_out)
                 state["total"] = tot
             else:
-                state["total"] = fdist.compress_gather(pieces(), dist, rank_bytes, block, args.nsub)
+                state["total"] = fdist.compress_gather(pieces(), dist, rank_bytes, block, args.nsub,
+                                                       device=None if gloo else dev)
             return
         compress()
         seg_len = ctx.read_out_len() if n else 0
@@ -202,10 +276,8 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
             state["total"] = seg_len
             return
         if args.fcx_dist is not None:   # C++ RCCL path: sizes all-gather + gather / all-gather-v
-            import my_compress_amd as mc2
-
             dst = d_out if concat == "gather" else whole
-            mode = mc2.DIST_GATHER if concat == "gather" else mc2.DIST_ALLGATHER
+            mode = mc.DIST_GATHER if concat == "gather" else mc.DIST_ALLGATHER
             state["total"] = args.fcx_dist.concat(d_out.data_ptr(), seg_len, dst.data_ptr(), dst.numel(), mode, sid)
             state["seg"] = seg_len
             return
@@ -256,15 +328,23 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     }
     if concat != "none":
         res["concat_ms_per_step"] = res["ms_per_step"] - res["compress_only"]["ms_per_step"]
-        res["concat_impl"] = ("fcx_dist (C++ RCCL)" if args.fcx_dist is not None else
-                              f"torch.distributed ({dist.get_backend()})")
+        res["concat_impl"] = (f"fcx_dist (C++, {args.fcx_dist.transport()} transport)" if args.fcx_dist is not None
+                              else f"torch.distributed ({dist.get_backend()})")
         res["partition"] = {"share0_ppm": share0, "rank_bytes": rank_bytes,
                             "nsub": args.nsub if concat == "pipe" else None}
         if concat == "pipe" and scaling == "strong":
-            res["partition"]["model_ms"] = fdist.step_model_ms(
+            res["partition"]["model_ms_assumed_link"] = fdist.step_model_ms(
                 (share0 / 1e6) if share0 else 1.0 / world, world, fdist.COMPRESS_MS_PER_GIB.get(kind, 14.1),
                 fdist.RATIO.get(kind, 1.0), args.link_gbps, args.nsub, gib=n_global / GiB)
-            res["partition"]["model_link_gbps"] = args.link_gbps
+            res["partition"]["assumed_link_gbps"] = args.link_gbps
+            if calib is not None:
+                res["partition"]["calibration"] = calib
+                res["partition"]["measured_link_gbps"] = calib["link_gbps"]
+                res["partition"]["model_ms"] = calib["model_ms"]
+                res["partition"]["source"] = "measured (one warmup step: compress rate, ratio, gather link rate)"
+            else:
+                res["partition"]["source"] = ("--share0" if args.share0_ppm >= 0 else
+                                              f"step model at the assumed {args.link_gbps} GB/s link")
     stats = ctx.stats() if n else {"tokens": 0, "matches": 0, "lazy_evals": 0, "lazy_tiles": 0}
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
@@ -277,6 +357,7 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     if not args.no_decode and (main_leg or world == 1):
         res["decode"] = decode_leg(d_out, seg_len, n, block, d_in, args, dev, dist, world)
     ctx.close()
+    S.clear()
     del d_in, d_out, whole
     torch.cuda.empty_cache()
     return res
@@ -609,7 +690,9 @@ def main():
                     help="pipe: rank 0's share of the blocks in ppm (-1 = the step model's choice)")
     ap.add_argument("--nsub", type=int, default=4, help="pipe: sub-batches per peer")
     ap.add_argument("--link-gbps", type=float, default=64.0,
-                    help="pipe: xGMI GB/s per link and direction assumed by the partition model")
+                    help="pipe: xGMI GB/s per link and direction assumed by the partition model before calibration")
+    ap.add_argument("--no-calibrate", dest="calibrate", action="store_false",
+                    help="pipe, N > 1: keep the modelled share0 (default: re-partition from one measured warmup step)")
     ap.add_argument("--concat-impl", default="fcx", choices=["fcx", "torch"],
                     help="fcx: the C++ RCCL path (fcx_dist_concat); torch: torch.distributed P2P / broadcast")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
@@ -732,6 +815,24 @@ def main():
             line["weak"] = {k: weak[k] for k in keep + ["rank_segments_bit_exact", "global_bytes"] if k in weak}
             line["weak"]["workload"] = (f"BASELINE config 4 sharding: rank r = bytes [r GiB, (r+1) GiB) of the "
                                         f"seed-4 rand stream, {world} GiB total, segments gathered to rank 0")
+        # a compact per-leg summary as the LAST key, so a reader that keeps only the line's tail
+        # (the driver keeps 8 KB) still sees every leg
+        summ = {}
+
+        def brief(name, v, lr=None):
+            rf, cb = v.get("roofline") or {}, v.get("cpu_baseline") or {}
+            summ[name] = {"value": round(v["value"], 1), "ms": round(v["ms_per_step"], 3),
+                          "bit_exact": v.get("bit_exact_vs_reference"),
+                          "frac": round(rf["frac"], 4) if rf.get("frac") else None,
+                          "path_frac": round(rf["path_frac"], 4) if rf.get("path_frac") else None,
+                          "cpu_MBps": round(cb["value"], 1) if cb.get("value") else None}
+
+        brief(args.kind, line)
+        for name in legs:
+            brief(name, line[name])
+        if "weak" in line:
+            brief("weak", line["weak"])
+        line["legs"] = summ
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -254,9 +254,10 @@ int fcx_dist_concat(fcx_dist *d, int local, const uint8_t *d_seg, uint64_t seg_l
  * handle keeps, then moves them behind its own segment: d_out[0, *total) on rank 0 is every
  * rank's [u32 len][payload] records in block order (capacity >= fcx_shard_bound of the whole
  * input).  A peer whose compress fails sends failure words instead of pieces, so rank 0 always
- * completes the exchange and returns the error.  *total: the concatenation on rank 0, the bytes
- * sent on a peer.  Collective over the job; `stream` is the compress stream; returns after both
- * streams are synchronised. */
+ * completes the exchange; rank 0 then sends the job's verdict to every peer, so every rank
+ * returns an error when any rank failed.  *total: the concatenation on rank 0, the bytes sent on
+ * a peer.  Collective over the job; `stream` is the compress stream; returns after both streams
+ * are synchronised. */
 #define FCX_DIST_MAX_SUB 64u
 int fcx_dist_compress_gather(fcx_dist *d, fcx_ctx *ctx, const uint8_t *d_in, uint64_t n, const uint64_t *rank_bytes,
                              uint32_t nsub, uint8_t *d_out, uint64_t cap, uint64_t *total, void *stream);
@@ -268,6 +269,29 @@ uint64_t fcx_dist_gather_bound(uint64_t n, uint32_t block_bytes, uint32_t nsub);
  * RCCL and copied to `out` ([u32 len][payload] records, no header); *out_len = bytes. */
 int fcx_dist_compress_host(fcx_dist *d, const uint8_t *in, uint64_t n, uint32_t block_bytes, uint64_t round_bytes,
                            uint8_t *out, uint64_t cap, uint64_t *out_len);
+/* name of the transport under a handle: "rccl" or "loopback" */
+const char *fcx_dist_transport(fcx_dist *d);
+
+/* ---- loopback transport: the protocols above between thread ranks of one process ------
+ * The multi-rank protocols (fcx_dist_concat, fcx_dist_compress_gather, fcx_dist_compress_host)
+ * talk to a transport seam (group start/end, send/recv of device bytes, all-gather,
+ * broadcast); RCCL is the product transport.  The loopback transport runs the same protocol
+ * code between host threads of one process on one device -- each thread rank with its own
+ * fcx_dist, fcx_ctx and streams -- so the N > 1 exchange runs on a one-GPU box: a matched
+ * send/recv pair is one device-to-device copy on the hub's stream, ordered after both sides'
+ * stream positions, and both streams wait for it.  An operation left unmatched for
+ * timeout_ms (0 = 60 s) aborts the hub, and every rank then fails instead of hanging. */
+typedef struct fcx_loop fcx_loop;
+int fcx_loop_create(fcx_loop **hub, int nranks, int device, uint32_t timeout_ms);
+/* drops the creator's reference; the hub lives until its last fcx_dist is destroyed */
+void fcx_loop_destroy(fcx_loop *hub);
+/* rank `rank` of the hub's job, one rank per handle (the fcx_dist_init_rank form) */
+int fcx_dist_init_loop(fcx_dist **d, fcx_loop *hub, int rank);
+/* every rank of an nranks job in one handle on one device (the fcx_dist_init_local form) */
+int fcx_dist_init_loop_local(fcx_dist **d, int nranks, int device, uint32_t timeout_ms);
+/* Testing: a peer of fcx_dist_compress_gather treats sub-batch `piece` as failed after the
+ * earlier pieces are queued (as device error bits would); -1 = off. */
+int fcx_dist_debug_fail(fcx_dist *d, int piece);
 
 const char *fcx_last_error(void);
 const char *fcx_version(void);

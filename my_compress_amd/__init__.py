@@ -121,6 +121,15 @@ def lib():
                                   ctypes.c_uint64, P64, ctypes.c_int, ctypes.c_void_p]
     L.fcx_dist_compress_host.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                          c_u8p, ctypes.c_uint64, P64]
+    L.fcx_dist_transport.argtypes = [ctypes.c_void_p]
+    L.fcx_dist_transport.restype = ctypes.c_char_p
+    L.fcx_loop_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
+    L.fcx_loop_destroy.argtypes = [ctypes.c_void_p]
+    L.fcx_loop_destroy.restype = None
+    L.fcx_dist_init_loop.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_int]
+    L.fcx_dist_init_loop_local.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_uint32]
+    L.fcx_dist_debug_fail.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.fcx_last_error.restype = ctypes.c_char_p
     L.fcx_version.restype = ctypes.c_char_p
     _lib = L
@@ -446,10 +455,33 @@ def dist_unique_id() -> bytes:
     return buf.raw
 
 
+class Loop:
+    """fcx_loop: the in-process loopback transport's hub (include/fcx.h).  Thread ranks on one
+    device run the multi-rank protocols over it: Dist.loop(hub, r) per thread rank."""
+
+    def __init__(self, nranks: int, device: int = 0, timeout_ms: int = 60000):
+        self._h = ctypes.c_void_p()
+        _check(lib().fcx_loop_create(ctypes.byref(self._h), nranks, device, timeout_ms), "fcx_loop_create")
+        self.nranks = nranks
+
+    def close(self):
+        if self._h:
+            lib().fcx_loop_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Dist:
-    """fcx_dist: RCCL communicator(s) of the multi-GPU compress path.
+    """fcx_dist: communicator(s) of the multi-GPU compress path.
     Dist.local([0, 1, ...]) drives several devices from this process (the CLI's -g N);
-    Dist.rank(n, r, uid, device) is one rank of a process-per-GPU job."""
+    Dist.rank(n, r, uid, device) is one rank of a process-per-GPU job (RCCL);
+    Dist.loop(hub, r) / Dist.loop_local(n, device) are the same forms over the loopback
+    transport (thread ranks of one process on one device)."""
 
     def __init__(self, handle):
         self._h = handle
@@ -466,6 +498,25 @@ class Dist:
         h = ctypes.c_void_p()
         _check(lib().fcx_dist_init_rank(ctypes.byref(h), nranks, rank, uid, device), "fcx_dist_init_rank")
         return cls(h)
+
+    @classmethod
+    def loop(cls, hub: "Loop", rank: int):
+        h = ctypes.c_void_p()
+        _check(lib().fcx_dist_init_loop(ctypes.byref(h), hub._h, rank), "fcx_dist_init_loop")
+        return cls(h)
+
+    @classmethod
+    def loop_local(cls, nranks: int, device: int = 0, timeout_ms: int = 60000):
+        h = ctypes.c_void_p()
+        _check(lib().fcx_dist_init_loop_local(ctypes.byref(h), nranks, device, timeout_ms), "fcx_dist_init_loop_local")
+        return cls(h)
+
+    def transport(self) -> str:
+        return lib().fcx_dist_transport(self._h).decode()
+
+    def debug_fail(self, piece: int):
+        """testing: as a peer of compress_gather, treat sub-batch `piece` as failed (-1 = off)"""
+        _check(lib().fcx_dist_debug_fail(self._h, piece), "fcx_dist_debug_fail")
 
     def close(self):
         if self._h:

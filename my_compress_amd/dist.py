@@ -91,6 +91,36 @@ def gather_share_ppm(world: int, kind: str = "rand", link_gbps: float = 64.0, ns
     return best
 
 
+def calibrate_share(dist, kind: str, nsub: int, c_ms_per_gib: float, in_bytes: int, out_bytes: int, probe,
+                    device="cpu", group=None) -> dict:
+    """the gather-aware share from one warmup step's measurements instead of assumed rates.
+    Every rank passes its measured compress ms per GiB, its shard's input bytes and its compressed
+    segment's bytes; probe() gathers every peer's segment to rank 0 over the job's transport (the
+    real exchange pattern: all peers send at once, each over its own link) and returns its seconds
+    (rank 0's value is used).  The link rate is the largest peer segment over that time; the compress
+    rate is the slowest rank's; the ratio is the job's.  Returns, identically on every rank:
+    share0_ppm (the step model's choice with the measured figures), link_gbps, c_ms_per_gib, ratio,
+    probe_ms, probe_bytes (the largest peer segment) and the model's predicted step ms."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    mx = torch.tensor([float(c_ms_per_gib), float(out_bytes if rank else 0)], dtype=torch.float64, device=device)
+    sm = torch.tensor([float(in_bytes), float(out_bytes)], dtype=torch.float64, device=device)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM, group=group)
+    secs = torch.tensor([float(probe())], dtype=torch.float64, device=device)
+    dist.broadcast(secs, 0, group=group)
+    c_ms, peer_bytes = float(mx[0]), float(mx[1])
+    ratio = float(sm[1]) / max(float(sm[0]), 1.0)
+    t = max(float(secs[0]), 1e-6)
+    link = peer_bytes / t / 1e9 if peer_bytes > 0 else float("inf")
+    link_m = min(link, 1e4)   # (no peer bytes: the exchange costs nothing, the model wants a finite rate)
+    share = gather_share_ppm(world, kind, link_m, nsub, c_ms=c_ms, ratio=ratio)
+    gib = float(sm[0]) / (1 << 30)
+    return {"share0_ppm": share, "link_gbps": link, "c_ms_per_gib": c_ms, "ratio": ratio, "probe_ms": t * 1e3,
+            "probe_bytes": int(peer_bytes),
+            "model_ms": step_model_ms(share / 1e6, world, c_ms, ratio, link_m, nsub, gib=gib)}
+
+
 def exchange_sizes(seg_len: int, dist, device, group=None):
     """all-gather of the per-rank segment sizes; returns (sizes, offsets) in rank order"""
     world = dist.get_world_size(group)
@@ -148,7 +178,8 @@ def allgather_segments(seg: torch.Tensor, out: torch.Tensor, sizes, offs, dist, 
     return sum(sizes)
 
 
-def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=None, out=None, group=None):
+def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=None, out=None, group=None,
+                    device=None):
     """fcx_dist_compress_gather's protocol over torch.distributed (the `--concat-impl torch` path
     and the gloo tests).  A peer passes `pieces`, an iterable of its nsub sub-batch segments in
     order (uint8 tensors, e.g. compressed one by one as they are consumed): each is sent as it is
@@ -156,11 +187,13 @@ def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=N
     segment `own` (already at out[:len], or copied there) and `out` (>= the whole
     concatenation); per round s it receives every peer's length pair, then every peer's bytes
     into a staging region per peer, and finally moves them behind its own segment in rank order.
-    A peer that fails sends (-1, 1) for this and every later round.  Returns the concatenated
-    length on rank 0, the bytes sent on a peer."""
+    A peer that fails sends (-1, 1) for this and every later round.  Rank 0 then sends the job's
+    verdict (0 or 1) to every peer, so every rank raises when any rank failed.  `device`: where a
+    peer's control words live (its pieces' device; required under nccl, which cannot send CPU
+    tensors).  Returns the concatenated length on rank 0, the bytes sent on a peer."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    dev = out.device if out is not None else torch.device("cpu")
+    dev = out.device if out is not None else torch.device(device if device is not None else "cpu")
     if rank != 0:
         sent, failed = 0, False
         it = iter(pieces)
@@ -172,14 +205,17 @@ def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=N
                 except Exception:   # a failed compress: publish it, keep the protocol
                     failed = True
             n = 0 if failed else int(seg.numel())
-            words = torch.tensor([-1, 1] if failed else [n, 0], dtype=torch.int64, device=seg.device if seg is not None
-                                 else dev)
+            words = torch.tensor([-1, 1] if failed else [n, 0], dtype=torch.int64, device=dev)
             dist.send(words, 0, group)
             if n:
                 dist.send(seg.contiguous(), 0, group)
             sent += n
+        verdict = torch.zeros(1, dtype=torch.int64, device=dev)
+        dist.recv(verdict, 0, group)
         if failed:
             raise RuntimeError("compress_gather: this rank's compress failed")
+        if int(verdict.item()):
+            raise RuntimeError("compress_gather: rank 0 reports the job failed")
         return sent
     stage_cap = [0] + [sum(2 * (hi - lo) + 4096 * ((hi - lo + block_bytes - 1) // block_bytes) + 64
                            for lo, hi in piece_ranges(rank_bytes[r], block_bytes, nsub)) for r in range(1, world)]
@@ -204,6 +240,11 @@ def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=N
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+    verdict = torch.tensor([1 if err else 0], dtype=torch.int64, device=dev)
+    ops = [dist.P2POp(dist.isend, verdict, r, group) for r in range(1, world)]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
     if err:
         raise RuntimeError("compress_gather: " + err)
     n_own = int(own.numel()) if own is not None else 0

@@ -159,9 +159,10 @@ def test_pipelined_gather_uneven_partition(world):
     results = mgr.dict()
     mp.spawn(_gather_worker, args=(world, _free_port(), cases, results), nprocs=world, join=True)
     for idx, (spec, block, share, nsub, fail_rank) in enumerate(cases):
-        if fail_rank >= 0:
+        if fail_rank >= 0:   # every rank learns the job failed (rank 0's verdict), nobody hangs
             assert str(results[(idx, 0)]).startswith("error:") and "failed" in results[(idx, 0)], results[(idx, 0)]
-            assert str(results[(idx, fail_rank)]).startswith("error:")
+            for r in range(world):
+                assert str(results[(idx, r)]).startswith("error:"), (r, results[(idx, r)])
             continue
         data = inputs.make(spec)
         assert results[(idx, 0)] == oracle.compress_file(data, block), (idx, spec, share, nsub)
@@ -218,3 +219,54 @@ def test_step_model_is_monotone_by_design():
         even = fdist.step_model_ms(0.5, 2, c, r, 64.0, 1)
         if kind == "rand":
             assert even > t[0]
+
+
+# ---- calibration of the gather-aware split (bench.py --concat pipe at N > 1) -------------------
+def _calib_worker(rank, world, port, results):
+    import time
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # a deterministic probe: rank 0's time is the one used
+        fixed = fdist.calibrate_share(dist, "rand", 4, 4.5 + rank, 100 << 20, (101 << 20) + rank * 1000,
+                                      lambda: 0.004 if rank == 0 else 9.0)
+        # the real pattern over gloo: every peer's segment to rank 0 at once
+        seg = torch.full(((3 << 20) * rank,), 7, dtype=torch.uint8)
+
+        def probe():
+            sizes, offs = fdist.exchange_sizes(seg.numel(), dist, "cpu")
+            buf = torch.empty(sum(sizes) + 1, dtype=torch.uint8)
+            t0 = time.perf_counter()
+            fdist.gather_segments(seg, buf, sizes, offs, dist, 0)
+            return time.perf_counter() - t0
+
+        real = fdist.calibrate_share(dist, "text", 4, 14.0, 64 << 20, seg.numel(), probe)
+        results[rank] = (fixed, real)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_calibrated_share_gloo(world):
+    """every rank derives the same share from the measured figures: the slowest rank's compress
+    rate, the job's ratio and the gather link rate of rank 0's probe"""
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_calib_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+    fixed = [results[r][0] for r in range(world)]
+    real = [results[r][1] for r in range(world)]
+    assert all(f == fixed[0] for f in fixed) and all(x == real[0] for x in real)
+    f = fixed[0]
+    peer_bytes = (101 << 20) + (world - 1) * 1000
+    assert f["c_ms_per_gib"] == 4.5 + world - 1 and f["probe_bytes"] == peer_bytes
+    assert abs(f["link_gbps"] - peer_bytes / 0.004 / 1e9) < 1e-9
+    ratio = sum((101 << 20) + r * 1000 for r in range(world)) / (world * (100 << 20))
+    assert abs(f["ratio"] - ratio) < 1e-12
+    assert f["share0_ppm"] == fdist.gather_share_ppm(world, "rand", f["link_gbps"], 4, c_ms=f["c_ms_per_gib"],
+                                                     ratio=ratio)
+    r = real[0]
+    assert 0 < r["share0_ppm"] < 1_000_000 and r["link_gbps"] > 0 and r["probe_ms"] > 0
+    assert r["probe_bytes"] == (3 << 20) * (world - 1)
