@@ -19,7 +19,7 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *sdesc, hipStream_t st,
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *sdesc, uint32_t *err, hipStream_t st,
                   hipEvent_t *ev, uint32_t emit_dbg = 0);
 void launch_entropy(const Layout &L, BlockInfo *binfo, uint8_t *s0, uint8_t *s1, uint8_t *s2, uint8_t *s3,
                     const uint16_t *thist, uint32_t *ctab,
@@ -363,7 +363,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         launch_parse(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
                      c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 12 * t0,
                      c->tile_off + 3 * t0, c->tconv + t0, c->binfo + b0, sg_s[0], sg_s[1], sg_s[2], sg_s[3],
-                     c->thist + t0 * 256, c->sdesc + b0 * ((c->B + kCharSeg - 1) / kCharSeg), sg, ev ? ev + 3 : nullptr,
+                     c->thist + t0 * 256, c->sdesc + b0 * ((c->B + kCharSeg - 1) / kCharSeg), err, sg, ev ? ev + 3 : nullptr,
                      c->emit_dbg);
         if (c->emit_dbg & 0xFFFFu) {   // (development: k_emit's timing exits leave invalid streams; stop here)
             if (ev)

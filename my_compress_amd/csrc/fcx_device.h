@@ -53,6 +53,7 @@ constexpr uint32_t kRmSpan = 512;                // run-mode tiles keep m[] rows
 constexpr uint32_t kTileMatches = kTile / 4;     // compact match list slots per tile (a match covers >= 4)
 constexpr uint32_t kConvAll = 0xFFFFu;           // tile conv record: k_emit takes every m from m[]
 constexpr uint32_t kCharSeg = 64;                    // chars per segment descriptor (one k_encode lane's symbols)
+constexpr uint32_t kErrScratch = 8u;                 // device error bit: inconsistent per-tile scratch (k_emit)
 constexpr uint32_t kCdMixed = 0xFFFFFFFFu;       // chars segment descriptor: not a run of input bytes
 
 // per-block results of the parse/emit stage

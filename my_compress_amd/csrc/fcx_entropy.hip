@@ -499,7 +499,10 @@ __global__ __launch_bounds__(kEncT) __attribute__((amdgpu_waves_per_eu(8))) void
     const uint32_t errv = *err;
     const BlockInfo &bi = binfo[b];
     // chars: is this lane's segment a run of input bytes (k_emit's descriptor)?
-    const uint32_t cd = s == 1 ? sdesc[(uint64_t)b * ((L.B + kCharSeg - 1) / kCharSeg) + c * (kChunk / kCharSeg) + tid] : kCdMixed;
+    // (the last chunk of a block whose size is not a multiple of kChunk has lanes past the block's
+    // descriptors: they hold no symbols and read none)
+    const uint32_t nseg = (L.B + kCharSeg - 1) / kCharSeg, seg = c * (kChunk / kCharSeg) + tid;
+    const uint32_t cd = s == 1 && seg < nseg ? sdesc[(uint64_t)b * nseg + seg] : kCdMixed;
     const uint32_t len = bi.slen[s], c0 = c * kChunk;
     if (errv || !stream_active(bi, s) || c0 >= len) return;
     const uint32_t c1 = min(len, c0 + kChunk);

@@ -396,13 +396,15 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                 sti[lane][0] = tq[0]; sti[lane][1] = tq[1]; sti[lane][2] = tq[2];
                 sti[lane][3] = tq[3]; sti[lane][4] = tq[4];
                 const uint64_t f0 = fq[0];
-                sti[lane][5] = (uint32_t)f0;
+                // (nmod <= kResW by construction; clamped so that a bad record cannot index past
+                // the tile's chain words)
+                const uint32_t nmod = min((uint32_t)(f0 >> 16) & 0xFFu, kResW);
+                sti[lane][5] = ((uint32_t)f0 & 0xFFFFu) | (nmod << 16);
                 if (f0 & 1ull) {
                     const uint64_t f1 = fq[1];
                     sfp[lane][0] = (uint32_t)f1; sfp[lane][1] = (uint32_t)(f1 >> 32);
                     const uint64_t f2 = fq[2];
                     sfp[lane][2] = (uint32_t)f2; sfp[lane][3] = (uint32_t)fq[3]; sfp[lane][4] = (uint32_t)(f2 >> 32);
-                    const uint32_t nmod = (uint32_t)(f0 >> 16) & 0xFFu;
                     for (uint32_t u = 0; u < nmod; u++) sfw[lane][u] = fq[4 + u];
                 }
             }
@@ -770,7 +772,8 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
                                               const uint32_t *__restrict__ tconv, const uint32_t *__restrict__ tinfo,
                                               uint8_t *__restrict__ s_flags, uint8_t *__restrict__ s_chars,
                                               uint8_t *__restrict__ s_p, uint8_t *__restrict__ s_golomb,
-                                              uint16_t *__restrict__ thist, uint32_t *__restrict__ sdesc, uint32_t dbg_in) {
+                                              uint16_t *__restrict__ thist, uint32_t *__restrict__ sdesc,
+                                              uint32_t *__restrict__ err, uint32_t dbg_in) {
     const uint32_t dbg = kDev ? dbg_in : 0u;
     __shared__ uint32_t sh[16];
     __shared__ uint32_t hc[256];             // this tile's chars counts
@@ -796,6 +799,14 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     const uint32_t cv = tconv[tix];
     const bool uni = (tinfo[8 * tix] & kTileUniform) != 0;   // m = m_uniform, no rows
     const uint32_t nspec = tinfo[8 * tix + 3];   // match tokens of the speculative chain (its compact list)
+    // the tile's offsets and counts come from scratch the earlier kernels wrote: one inconsistent
+    // value (a kernel that did not run, a bug) sets an error bit instead of indexing the streams
+    // or the match list out of bounds (uniform values: scalar compares)
+    if (tk1 > blen || tok0 > tk1 || tk1 - tok0 > t1 - t0 || mi0 > mk1 || mk1 - mi0 > tk1 - tok0 || mk1 > tk1 ||
+        nspec > kTileMatches || (cv >> 16) > kTileMatches || g0 > 8u * L.sstride[3]) {
+        if (tid == 0) atomicOr(err, kErrScratch);
+        return;
+    }
     const uint32_t s = t0 + tid * 16;   // this lane's 16 positions: one quarter of a chain word
     uint64_t cwv = 0, mbv = 0;
     if (s < t1) {
@@ -1058,7 +1069,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
-                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *sdesc, hipStream_t st,
+                  uint8_t *s_p, uint8_t *s_golomb, uint16_t *thist, uint32_t *sdesc, uint32_t *err, hipStream_t st,
                   hipEvent_t *ev, uint32_t emit_dbg) {
     const uint32_t ntiles = L.nblocks * L.tpb;
     hipLaunchKernelGGL(k_resolve, dim3(ntiles), dim3(64), 0, st, L, m, mbits, chain, chain_pfx, tinfo, fp);
@@ -1068,10 +1079,10 @@ void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_
     emit_dbg &= 0xFFFFu;   // (bits 16.. are k_tree's)
     if (emit_dbg == 0)
         hipLaunchKernelGGL(k_emit<false>, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok,
-                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, sdesc, 0u);
+                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, sdesc, err, 0u);
     else
         hipLaunchKernelGGL(k_emit<true>, dim3(ntiles), dim3(256), 0, st, in, L, m, mbits, chain, tile_off, binfo, mtok,
-                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, sdesc, emit_dbg);
+                           tconv, tinfo, s_flags, s_chars, s_p, s_golomb, thist, sdesc, err, emit_dbg);
     if (ev) (void)hipEventRecord(ev[1], st);
 }
 

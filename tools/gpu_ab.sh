@@ -1,6 +1,12 @@
 # A/B of library variants: devbench stage times per leg for lib/libfcx.so (A) and each
 # lib/libfcx_<V>.so in $VARS (FCX_LIB), e.g. VARS="x y" KINDS="rand text c3" bash tools/gpu_ab.sh
 set -u
+# timing-exit builds (tools/phase_libs.sh: libfcx_x<N>.so, FCX_MATCH_EXIT) leave the scratch the later
+# kernels read unwritten: they are for the kernel-alone timing (tools/gpu_match_phases.sh), never the
+# whole pipeline run here
+for v in ${VARS:-b}; do
+  case $v in x*) echo "gpu_ab.sh: refusing timing-exit variant libfcx_$v.so (use tools/gpu_match_phases.sh)" >&2; exit 2;; esac
+done
 for leg in ${KINDS:-rand text dna runs}; do
   case $leg in
     text) a="--kind text --seed 3 --mib 1024 --check hl_text_1GiB";;
