@@ -82,6 +82,39 @@ __global__ __launch_bounds__(kT, 8) void k_persist_pf(const uint8_t *in, uint64_
     }
 }
 
+// k_encode's shape: a 128-lane workgroup per 8192-byte chunk, 64 bytes per lane (4 x 16 B in, 4 x 16 B out)
+template <int kLanes, int kPer>
+__global__ __launch_bounds__(kLanes) void k_copy_grid(const uint4 *in, uint4 *out, uint64_t n16) {
+    const uint64_t base = (uint64_t)blockIdx.x * kLanes * kPer;
+    uint4 v[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+        const uint64_t i = base + (uint64_t)q * kLanes + threadIdx.x;
+        v[q] = i < n16 ? in[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+        const uint64_t i = base + (uint64_t)q * kLanes + threadIdx.x;
+        if (i < n16) out[i] = make_uint4(v[q].y, v[q].x, v[q].w, v[q].z);
+    }
+}
+template <int kLanes, int kPer>
+__global__ __launch_bounds__(kLanes) void k_copy_persist(const uint4 *in, uint4 *out, uint64_t n16) {
+    for (uint64_t base = (uint64_t)blockIdx.x * kLanes * kPer; base < n16; base += (uint64_t)gridDim.x * kLanes * kPer) {
+        uint4 v[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            const uint64_t i = base + (uint64_t)q * kLanes + threadIdx.x;
+            v[q] = i < n16 ? in[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            const uint64_t i = base + (uint64_t)q * kLanes + threadIdx.x;
+            if (i < n16) out[i] = make_uint4(v[q].y, v[q].x, v[q].w, v[q].z);
+        }
+    }
+}
+
 int main(int argc, char **argv) {
     const uint64_t n = 1ull << 30;
     const uint32_t ntiles = (uint32_t)(n / kTile);
@@ -119,5 +152,22 @@ int main(int argc, char **argv) {
         snprintf(nm, sizeof nm, "persistent+prefetch %u WGs", g);
         timeit(nm, [&] { hipLaunchKernelGGL(k_persist_pf, dim3(g), dim3(kT), 0, 0, in, n, out, ntiles); });
     }
+    uint8_t *o2;
+    (void)hipMalloc(&o2, n + 64);
+    const uint64_t n16 = n / 16;
+    timeit("hipMemcpy D2D 1 GiB", [&] { (void)hipMemcpyAsync(o2, in, n, hipMemcpyDeviceToDevice, 0); });
+    timeit("copy grid 128x(4x16B)", [&] {
+        hipLaunchKernelGGL((k_copy_grid<128, 4>), dim3((uint32_t)(n16 / 512)), dim3(128), 0, 0, (const uint4 *)in, (uint4 *)o2, n16); });
+    timeit("copy grid 256x(4x16B)", [&] {
+        hipLaunchKernelGGL((k_copy_grid<256, 4>), dim3((uint32_t)(n16 / 1024)), dim3(256), 0, 0, (const uint4 *)in, (uint4 *)o2, n16); });
+    timeit("copy grid 256x(8x16B)", [&] {
+        hipLaunchKernelGGL((k_copy_grid<256, 8>), dim3((uint32_t)(n16 / 2048)), dim3(256), 0, 0, (const uint4 *)in, (uint4 *)o2, n16); });
+    for (int per : {8, 16, 32}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "copy persistent 256x4 x%d/CU", per);
+        timeit(nm, [&] { hipLaunchKernelGGL((k_copy_persist<256, 4>), dim3((uint32_t)(cus * per)), dim3(256), 0, 0,
+                                            (const uint4 *)in, (uint4 *)o2, n16); });
+    }
+    printf("(copy: 2 GiB of traffic per GiB)\n");
     return 0;
 }
