@@ -16,6 +16,8 @@
 namespace fcx {
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
                   uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
+void launch_match_k4(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                     uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -82,6 +84,8 @@ namespace fcx {
 void set_last_error(const std::string &m) { g_err = m; }
 }  // namespace fcx
 
+constexpr uint64_t kKeyProbe = 16;   // calls without a length read per read of the small-alphabet count
+
 struct fcx_ctx {
     int device = 0;
     uint32_t B = 0;
@@ -105,8 +109,12 @@ struct fcx_ctx {
     uint32_t *ctab = nullptr;          // code table
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
-    uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits
-    uint64_t *host_words = nullptr;    // pinned mirror
+    uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits, [2] = small-alphabet
+                                       // blocks | blocks << 32 (k_tree)
+    uint64_t *host_words = nullptr;    // pinned mirror ([2]: refreshed by the length reads, and by an
+                                       // asynchronous copy every kKeyProbe-th call without one)
+    uint64_t calls = 0;
+    bool last_key4 = false;            // the last call ran the 4-byte-key match kernel
     // pipelined launch: the shard's blocks in groups, consecutive groups on two streams so
     // one group's serial / latency-bound kernels (stitch, tree, scan, emit, encode) overlap
     // the next group's match kernel; the record-offset scans stay in group order
@@ -116,6 +124,7 @@ struct fcx_ctx {
     // profiling
     bool profiling = false;
     uint32_t match_mode = 0;   // k_match tile-mode bits (fcx_ctx_set_match_mode)
+    int key4 = -1;             // match kernel: -1 = choose per call, 0 = 3-byte keys, 1 = 4-byte keys
     uint32_t emit_dbg = 0;     // k_emit development exits (fcx_debug_emit_bits; output invalid)
     hipEvent_t ev[kMaxGroups][kNumStages + 1] = {};
     uint32_t ngroups_timed = 0;
@@ -227,6 +236,7 @@ int fcx_ctx_create(fcx_ctx **out, int device, uint32_t block_bytes, uint64_t max
     c->B = block_bytes;
     e = hipHostMalloc((void **)&c->host_words, 64, hipHostMallocDefault);
     if (e != hipSuccess) { delete c; return hip_fail(e, "hipHostMalloc"); }
+    memset(c->host_words, 0, 64);   // (no small-alphabet blocks seen yet)
     e = hipMalloc((void **)&c->dev_words, 64);
     if (e != hipSuccess) { (void)hipHostFree(c->host_words); delete c; return hip_fail(e, "hipMalloc"); }
     for (uint32_t g = 0; g < kMaxGroups; g++)
@@ -262,7 +272,7 @@ int fcx_ctx_read_out_len(fcx_ctx *c, uint64_t *out_len) {
     if (!c || !out_len) return fail(FCX_ERR_ARG, "fcx_ctx_read_out_len: NULL");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 24, hipMemcpyDeviceToHost));
     const uint32_t e = (uint32_t)c->host_words[1];
     if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
     if (e) return fail(FCX_ERR_INTERNAL, "device invariant violated (error bits " + std::to_string(e) + ")");
@@ -278,8 +288,11 @@ int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
 
 int fcx_ctx_set_match_mode(fcx_ctx *c, int mode) {
     if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
-    if (mode < 0 || mode > 2) return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search) or 2 (run table)");
+    if (mode < 0 || mode > 4)
+        return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search), 2 (run table), "
+                                 "3 (3-byte-key kernel) or 4 (4-byte-key kernel)");
     c->match_mode = mode == 1 ? 4u | 128u : mode == 2 ? 8u : 0u;   // k_match dbg bits: all keep the output exact
+    c->key4 = mode == 0 ? -1 : mode == 4 ? 1 : 0;
     return FCX_OK;
 }
 
@@ -337,7 +350,15 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     c->timed = c->profiling;
     c->ngroups_timed = c->profiling ? G : 0;
 
-    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 16, st));
+    // match kernel: the 4-byte-key one when >= 90 % of the previous read-back call's blocks had
+    // small alphabets (dense 3-byte keys: 'ACGT' data); both give the same bytes
+    // (host_words[2] may be landing from an earlier call's copy: either value is a valid choice)
+    const uint64_t hw2 = __atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);
+    const uint64_t nsmall = hw2 & 0xFFFFFFFFu, nblk = hw2 >> 32;
+    const bool key4 = c->key4 >= 0 ? c->key4 == 1 : nblk && 10 * nsmall >= 9 * nblk;
+    auto match = key4 ? launch_match_k4 : launch_match;
+    c->last_key4 = key4;
+    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 24, st));
     if (G > 1) {
         HIP_TRY(hipEventRecord(c->gsync[0], st));
         for (auto s2 : c->gst) HIP_TRY(hipStreamWaitEvent(s2, c->gsync[0], 0));
@@ -356,7 +377,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
             HIP_TRY(hipEventRecord(ev[1], sg));   // (the memset above is not timed per group)
         }
         const uint8_t *gin = d_in + b0 * c->B;
-        launch_match(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
+        match(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
                      c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, sg,
                      c->match_mode);
         if (ev) HIP_TRY(hipEventRecord(ev[2], sg));
@@ -384,8 +405,10 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         }
     }
     HIP_TRY(hipGetLastError());
+    if (!out_len && c->key4 < 0 && c->calls++ % kKeyProbe == 0)
+        HIP_TRY(hipMemcpyAsync(c->host_words + 2, c->dev_words + 2, 8, hipMemcpyDeviceToHost, st));
     if (out_len) {
-        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 16, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 24, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         const uint32_t e = (uint32_t)c->host_words[1];
         if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
@@ -432,6 +455,9 @@ int fcx_debug_emit_bits(fcx_ctx *c, uint32_t bits) {
     return FCX_OK;
 }
 
+// testing only (not in fcx.h): the key width of the last call's match kernel (3 or 4)
+int fcx_debug_match_key(fcx_ctx *c) { return c ? (c->last_key4 ? 4 : 3) : 0; }
+
 // development only (not in fcx.h): the match kernel alone with experiment bits, for
 // per-phase timing (tools/matchphase.py); the context's scratch is left invalid
 int fcx_debug_match(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint32_t dbg, void *stream) {
@@ -440,7 +466,8 @@ int fcx_debug_match(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint32_t dbg, v
     int r = ensure_scratch(c, n);
     if (r) return r;
     const Layout L = make_layout(n, c->B);
-    launch_match(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok, (hipStream_t)stream, dbg);
+    (c->key4 == 1 ? launch_match_k4 : launch_match)(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok,
+                                                    (hipStream_t)stream, dbg);
     HIP_TRY(hipGetLastError());
     return FCX_OK;
 }

@@ -43,6 +43,22 @@
 #define FCX_MATCH_EXIT 0u   // development: a dbg timing-exit bit compiled into the product kernel (tools/phase_libs.sh)
 #endif
 
+// FCX_KEY4 (fcx_match_k4.hip): the same kernel with the bucket search over 4-byte keys, for shards of
+// dense keys (small alphabets such as 'ACGT' data: 64 distinct 3-byte keys, ~32 candidates per
+// query).  A match of length >= 4 shares its query's first four bytes, so the 4-byte bucket holds
+// every candidate of a longest match >= 4 (a quarter of the 3-byte candidates on 'ACGT' data); a
+// query without one takes the leftmost 3-byte match by a window scan.  The context picks this
+// translation unit per call from the previous call's share of small-alphabet blocks (k_tree);
+// both units give the same bytes.  The K3 unit's source is unchanged by the K4 branches below
+// (preprocessor): k_match's register allocation moves with any edit of its source.
+#ifndef FCX_KEY4
+#define FCX_KEY4 0
+#endif
+#if FCX_KEY4
+#define k_match k_match_k4
+#define launch_match launch_match_k4
+#endif
+
 namespace fcx {
 
 constexpr uint32_t kWinPos = kHalo + 1 + kTile;      // 6144 window positions per tile
@@ -87,6 +103,10 @@ static_assert(kRunBmWords <= 4 * 64, "prefix scan spans four waves");
 static_assert(kRunTableCap >= 1536, "run table");
 
 __device__ inline uint32_t key_mix(uint32_t key) { return (key * 0x9E3779B1u) & 0xFFFFFFu; }  // bijective mod 2^24
+#if FCX_KEY4
+__device__ inline uint32_t key_mix4(uint32_t key) { return (key * 0x9E3779B1u) >> 8; }   // 24 mixed bits of 4 bytes
+constexpr uint32_t kNeed3 = 0xFFFFFFFEu;   // query result: no 4-byte candidate, take the leftmost 3-byte match
+#endif
 
 // lanes below this one with their bit set in a wave mask
 __device__ inline uint32_t lanes_below(uint64_t m) {
@@ -939,8 +959,13 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 #pragma unroll
     for (uint32_t p = 0; p < kIns; p++) {
         ins_hr[p] = 0xFFFFFFFFu;
+#if FCX_KEY4
+        if (tid + kMT * p < min(npos, blen >= 4 ? blen - 3 - w0 : 0)) {   // j + 4 <= blen
+            const uint32_t h = key_mix4(lds_ld4(sdw, tid + kMT * p));
+#else
         if (tid + kMT * p < ins_end) {
             const uint32_t h = key_mix(lds_key3(sdw, tid + kMT * p));
+#endif
             const uint32_t bk = h >> (24 - kHashBits), sh = 16 * (bk & 1);
             const uint32_t old = atomicAdd(&hw[bk >> 1], 1u << sh);
             ins_hr[p] = (bk << 16) | ((h & 7u) << 13) | ((old >> sh) & 0x1FFFu);   // rank < 6144
@@ -952,7 +977,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         for (uint32_t r = 0; r < kQPL; r++) {
             // lo: the query is not inserted yet; its bucket comes from its key
             if ((qsl == 4 && p + 1 == r) || (qsl == 0 && p + 5 == r)) {
+#if FCX_KEY4
+                const uint32_t bk = key_mix4(lds_ld4(sdw, q0 + tid + kMT * r)) >> (24 - kHashBits);
+#else
                 const uint32_t bk = key_mix(lds_key3(sdw, q0 + tid + kMT * r)) >> (24 - kHashBits);
+#endif
                 snap[r] = (snap[r] & 0xFFFF0000u) | counter(bk);
             }
             if ((qsl == 4 && p == r + 5) || (qsl == 0 && p == r + 1)) {
@@ -1025,7 +1054,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                     qa[u] = lds_ld4(sdw, x);
                     qb[u] = lds_ld4(sdw, x + 4);
                     qc[u] = lds_ld4(sdw, x + 8);
+#if FCX_KEY4
+                    const uint32_t h = key_mix4(qa[u]);
+#else
                     const uint32_t h = key_mix(qa[u] & 0xFFFFFFu);
+#endif
                     const uint32_t bk = h >> (24 - kHashBits);
                     const uint32_t sn = snap[g + u];
                     const uint32_t b0 = h16[bk], b1 = h16[bk + 1];
@@ -1063,7 +1096,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                 const uint32_t wb = xe >> 2, sb = xe & 3;
                 const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1], w_2 = sdw[wb + 2], w_3 = sdw[wb + 3];
                 const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa[u];
+#if FCX_KEY4
+                if (d0) continue;   // 3-tag-bit collision: different key
+#else
                 if (d0 & 0xFFFFFFu) continue;   // 3-tag-bit collision: different key
+#endif
                 uint32_t Lc;
                 if (d0) Lc = 3;
                 else {
@@ -1134,11 +1171,19 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             const uint32_t wq = x >> 2, sq = x & 3;
             const uint32_t q_0 = sdw[wq], q_1 = sdw[wq + 1];
             const uint32_t qa1 = __builtin_amdgcn_alignbyte(q_1, q_0, sq);
+#if FCX_KEY4
+            if (((nd >> 13) & 7u) != (key_mix4(qa1) & 7u)) continue;
+#else
             if (((nd >> 13) & 7u) != (key_mix(qa1 & 0xFFFFFFu) & 7u)) continue;
+#endif
             const uint32_t wb = xe >> 2, sb = xe & 3;
             const uint32_t w_0 = sdw[wb], w_1 = sdw[wb + 1];
             const uint32_t d0 = __builtin_amdgcn_alignbyte(w_1, w_0, sb) ^ qa1;
+#if FCX_KEY4
+            if (d0) continue;
+#else
             if (d0 & 0xFFFFFFu) continue;
+#endif
             const uint32_t cap = min(kMaxL, blen - (w0 + x)) - 1;
             uint32_t Lc;
             if (d0) Lc = 3;
@@ -1183,11 +1228,37 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             if (x < npos) {
                 const uint32_t Lb = best[u] >> 13, xb = 8191u - (best[u] & 0x1FFFu);
                 if (rng[u] == 0xFFFFFFFFu) { res = kUnknown; s_unknown = 1; }
+#if FCX_KEY4
+                else if (Lb >= kMinL + 1) { res = m_pack(Lb, x - xb); s_match = 1; }
+                else if (((xpk[u] >> 13) & 0x1FFu) >= kMinL) res = kNeed3;   // (cap >= 3: a 3-byte match may exist)
+#else
                 else if (Lb >= kMinL) { res = m_pack(Lb, x - xb); s_match = 1; }
+#endif
             }
             rs[g + u] = res;
         }
     }
+#if FCX_KEY4
+    // queries without a 4-byte candidate: their longest match is < 4, so it is the leftmost 3-byte
+    // match in the window (the reference's leftmost-longest, capped at 3), found by a wave scan
+#pragma unroll
+    for (uint32_t r = 0; r < kQPL; r++) {
+        for (uint64_t nb = __ballot(rs[r] == kNeed3); nb; nb &= nb - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(nb);
+            const uint32_t x = q0 + 64 * wv + l + kMT * r;   // (lane l's query r)
+            const uint32_t key = lds_key3(sdw, x);
+            const uint32_t xlo = max(w0 + x, kWin) - kWin - w0;
+            uint32_t res = 0;
+            for (uint32_t j0 = xlo; j0 < x; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                const uint64_t hit = __ballot(j < x && lds_key3(sdw, j) == key);
+                if (hit) { res = m_pack(kMinL, x - (j0 + (uint32_t)__builtin_ctzll(hit))); break; }
+            }
+            if (lane == l) rs[r] = res;
+            if (res && lane == 0) s_match = 1;
+        }
+    }
+#endif
     __syncthreads();   // the search region is dead from here on; s_unknown is final
     {
         uint32_t *res_lds = region + kResLds;

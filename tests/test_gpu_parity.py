@@ -60,10 +60,11 @@ def test_golden_cases_bit_exact(golden, gpu_compress):
     assert not bad, f"GPU output differs from the reference on {bad}"
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 4])
 def test_golden_cases_forced_match_mode(golden, gpu_compress, mode):
     """every tile through one evaluation path of k_match (1: hash buckets + run table
-    for the unknowns, 2: run table for whole tiles): the output must not change"""
+    for the unknowns, 2: run table for whole tiles, 4: every call through the 4-byte-key
+    kernel, whatever the data): the output must not change"""
     bad = []
     for case in _cases(golden):
         if case["in_bytes"] > 1 << 20:
@@ -302,3 +303,60 @@ def test_cfg4_rank_segments(cuda):
     assert not bad, f"config-4 rank segments differ from the reference: {bad}"
     assert total == inputs.C4_FILE["bytes"]
     assert whole.hexdigest() == inputs.C4_FILE["out"]
+
+
+def _small_alphabet_mix(seed: int, n: int) -> bytes:
+    """small-alphabet data (dense 3-byte keys) next to text, random bytes, runs and periodic
+    stretches, so 3-byte-only matches, matches capped at block ends and every tile mode occur
+    in the 4-byte-key kernel"""
+    rng = random.Random(seed)
+    parts, left = [], n
+    while left > 0:
+        kind = rng.choice(["dna", "dna", "ac", "text", "rand", "runs", "period"])
+        ln = min(left, rng.randrange(3000, 60000))
+        if kind == "ac":   # two letters: every 3-byte key repeats constantly
+            parts.append(bytes(rng.choice(b"AC") for _ in range(ln)))
+        elif kind == "period":
+            unit = bytes(rng.choice(b"ACGT") for _ in range(rng.randrange(3, 9)))
+            parts.append((unit * (ln // len(unit) + 1))[:ln])
+        else:
+            parts.append(inputs.generate(kind, rng.randrange(1 << 30), ln))
+        left -= ln
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("block", [1 << 20, 65536, 5000])
+def test_key4_kernel_vs_oracle(cuda, block):
+    """the 4-byte-key match kernel (fcx_match_k4.hip): forced (mode 4) and chosen by the
+    context from its previous call (mode 0: 'ACGT' data switches from the second call on),
+    against the oracle on dna, mixed small-alphabet / text / random / periodic data and a
+    ragged tail"""
+    import ctypes
+
+    import torch
+
+    key = mc.lib().fcx_debug_match_key
+    key.argtypes, key.restype = [ctypes.c_void_p], ctypes.c_int
+    cases = [("dna", inputs.generate("dna", 6, 3 << 20)), ("mix", _small_alphabet_mix(5, 3 << 20)),
+             ("ragged", bytes(random.Random(7).choice(b"ACGT") for _ in range(100003)))]
+    for name, data in cases:
+        want = oracle.compress_file(data, block)
+        d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
+        cap = mc.shard_bound(len(data), block)
+        d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+        nb = (len(data) + block - 1) // block
+        for mode, calls in ((4, 1), (0, 3)):
+            ctx = mc.Context(0, block, len(data))
+            try:
+                ctx.set_match_mode(mode)
+                for call in range(calls):
+                    n = ctx.compress_shard(d_in.data_ptr(), len(data), d_out.data_ptr(), cap,
+                                           torch.cuda.current_stream().cuda_stream)
+                    got = mc.write_header(len(data), nb) + d_out[:n].cpu().numpy().tobytes()
+                    assert got == want, (name, block, mode, call)
+                    if mode == 4:
+                        assert key(ctx._h) == 4
+                    elif name == "dna" and block >= 65536:
+                        assert key(ctx._h) == (3 if call == 0 else 4), (block, call)
+            finally:
+                ctx.close()

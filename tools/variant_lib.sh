@@ -1,13 +1,13 @@
 # Development: build my_compress_amd/lib/libfcx_<name>.so with one source (default fcx_match) replaced by
-# a variant (the other objects from the current build), for tools/gpu_ab.sh.
-#   bash tools/variant_lib.sh name file.hip [fcx_parse]
+# a variant (the other objects from the current build), for tools/gpu_ab.sh; EXTRA: more compiler flags.
+#   [EXTRA="-mllvm ..."] bash tools/variant_lib.sh name file.hip [fcx_parse]
 set -eu
 name=$1; src=$(readlink -f $2); tgt=${3:-fcx_match}
 cd "$(dirname "$0")/../my_compress_amd/csrc"
 make -s
 mkdir -p build/v_$name
 cp $src ./fm_v_$name.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I../../include -I. -c fm_v_$name.hip \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I../../include -I. ${EXTRA:-} -c fm_v_$name.hip \
     -o build/v_$name/$tgt.o --save-temps 2>/dev/null
 python3 - fm_v_$name <<'PY'
 import re, sys
