@@ -130,9 +130,11 @@ int fcx_ctx_set_profiling(fcx_ctx *ctx, int enable);
 /* Testing: forces how the match kernel evaluates every tile of later calls —
  * 0 auto (default: run table for tiles of long runs, sparse search where few keys
  * repeat, else bucket search), 1 bucket search for every tile (unknown positions
- * via the run table / the stitch), 2 run table for whole tiles, 3 the 3-byte-key kernel
- * for every call, 4 the 4-byte-key kernel for every call (auto: the 4-byte-key kernel when
- * >= 90 % of the blocks of a recent call had small alphabets, e.g. 'ACGT' data: the call
+ * via the run table / the stitch), 2 run table for whole tiles, 3 the general kernel for
+ * every call, 4 the 4-byte-key kernel for every call, 5 the kernel without the repeat
+ * filter for every call (auto: the 4-byte-key kernel when >= 90 % of the blocks of a
+ * recent call had small alphabets, e.g. 'ACGT' data, else the no-filter kernel when
+ * >= 90 % were match-dense, e.g. text, else the general one; the recent call is the one
  * before when its length was read back, else the last of every 16th call).  The output is identical in every mode; only the speed
  * differs. */
 int fcx_ctx_set_match_mode(fcx_ctx *ctx, int mode);

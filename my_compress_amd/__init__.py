@@ -225,8 +225,8 @@ class Context:
         _check(lib().fcx_ctx_set_profiling(self._h, 1 if on else 0), "fcx_ctx_set_profiling")
 
     def set_match_mode(self, mode: int):
-        """testing: 0 auto, 1 bucket search, 2 run table for whole tiles, 3 the 3-byte-key
-        kernel, 4 the 4-byte-key kernel (same output; fcx.h)"""
+        """testing: 0 auto, 1 bucket search, 2 run table for whole tiles, 3 the general
+        kernel, 4 the 4-byte-key kernel, 5 the no-filter kernel (same output; fcx.h)"""
         _check(lib().fcx_ctx_set_match_mode(self._h, mode), "fcx_ctx_set_match_mode")
 
     def set_groups(self, groups: int):

@@ -18,6 +18,8 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
                   uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_match_k4(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
                      uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
+void launch_match_nf(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                     uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -84,7 +86,15 @@ namespace fcx {
 void set_last_error(const std::string &m) { g_err = m; }
 }  // namespace fcx
 
-constexpr uint64_t kKeyProbe = 16;   // calls without a length read per read of the small-alphabet count
+constexpr uint64_t kKeyProbe = 16;   // calls without a length read per read of the block-kind counts
+
+// the match kernel's translation units (fcx_match.hip, fcx_match_k4.hip, fcx_match_nf.hip)
+enum MatchKernel : int { kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2 };
+using MatchLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64_t *, uint64_t *, uint64_t *,
+                             uint32_t *, uint32_t *, hipStream_t, uint32_t);
+static MatchLaunch match_launcher(int k) {
+    return k == kMatchKey4 ? launch_match_k4 : k == kMatchNoFilter ? launch_match_nf : launch_match;
+}
 
 struct fcx_ctx {
     int device = 0;
@@ -110,11 +120,11 @@ struct fcx_ctx {
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
     uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits, [2] = small-alphabet
-                                       // blocks | blocks << 32 (k_tree)
-    uint64_t *host_words = nullptr;    // pinned mirror ([2]: refreshed by the length reads, and by an
+                                       // blocks | blocks << 32, [3] = match-dense blocks (k_tree, u32)
+    uint64_t *host_words = nullptr;    // pinned mirror ([2..3]: refreshed by the length reads, and by an
                                        // asynchronous copy every kKeyProbe-th call without one)
     uint64_t calls = 0;
-    bool last_key4 = false;            // the last call ran the 4-byte-key match kernel
+    int last_kernel = kMatchGeneral;   // the last call's match kernel
     // pipelined launch: the shard's blocks in groups, consecutive groups on two streams so
     // one group's serial / latency-bound kernels (stitch, tree, scan, emit, encode) overlap
     // the next group's match kernel; the record-offset scans stay in group order
@@ -124,7 +134,7 @@ struct fcx_ctx {
     // profiling
     bool profiling = false;
     uint32_t match_mode = 0;   // k_match tile-mode bits (fcx_ctx_set_match_mode)
-    int key4 = -1;             // match kernel: -1 = choose per call, 0 = 3-byte keys, 1 = 4-byte keys
+    int kernel = kMatchAuto;   // match kernel (MatchKernel): auto = chosen per call from the block kinds
     uint32_t emit_dbg = 0;     // k_emit development exits (fcx_debug_emit_bits; output invalid)
     hipEvent_t ev[kMaxGroups][kNumStages + 1] = {};
     uint32_t ngroups_timed = 0;
@@ -272,7 +282,7 @@ int fcx_ctx_read_out_len(fcx_ctx *c, uint64_t *out_len) {
     if (!c || !out_len) return fail(FCX_ERR_ARG, "fcx_ctx_read_out_len: NULL");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 24, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 32, hipMemcpyDeviceToHost));
     const uint32_t e = (uint32_t)c->host_words[1];
     if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
     if (e) return fail(FCX_ERR_INTERNAL, "device invariant violated (error bits " + std::to_string(e) + ")");
@@ -288,11 +298,11 @@ int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
 
 int fcx_ctx_set_match_mode(fcx_ctx *c, int mode) {
     if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
-    if (mode < 0 || mode > 4)
+    if (mode < 0 || mode > 5)
         return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search), 2 (run table), "
-                                 "3 (3-byte-key kernel) or 4 (4-byte-key kernel)");
+                                 "3 (general kernel), 4 (4-byte-key kernel) or 5 (no-filter kernel)");
     c->match_mode = mode == 1 ? 4u | 128u : mode == 2 ? 8u : 0u;   // k_match dbg bits: all keep the output exact
-    c->key4 = mode == 0 ? -1 : mode == 4 ? 1 : 0;
+    c->kernel = mode == 0 ? kMatchAuto : mode == 4 ? kMatchKey4 : mode == 5 ? kMatchNoFilter : kMatchGeneral;
     return FCX_OK;
 }
 
@@ -350,15 +360,23 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     c->timed = c->profiling;
     c->ngroups_timed = c->profiling ? G : 0;
 
-    // match kernel: the 4-byte-key one when >= 90 % of the previous read-back call's blocks had
-    // small alphabets (dense 3-byte keys: 'ACGT' data); both give the same bytes
-    // (host_words[2] may be landing from an earlier call's copy: either value is a valid choice)
-    const uint64_t hw2 = __atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);
-    const uint64_t nsmall = hw2 & 0xFFFFFFFFu, nblk = hw2 >> 32;
-    const bool key4 = c->key4 >= 0 ? c->key4 == 1 : nblk && 10 * nsmall >= 9 * nblk;
-    auto match = key4 ? launch_match_k4 : launch_match;
-    c->last_key4 = key4;
-    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 24, st));
+    // match kernel: when >= 90 % of a recent call's blocks had small alphabets (dense 3-byte keys:
+    // 'ACGT' data) the 4-byte-key one, else when >= 90 % were match-dense (text) the one without the
+    // repeat filter, else the general one; all give the same bytes.  (host_words[2..3]
+    // may be landing from an earlier call's copy: any value is a valid choice)
+    int kern = c->kernel;
+    if (kern == kMatchAuto) {
+        const uint64_t hw2 = __atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);
+        const uint64_t hw3 = __atomic_load_n(&c->host_words[3], __ATOMIC_RELAXED);
+        const uint64_t nsmall = hw2 & 0xFFFFFFFFu, nblk = hw2 >> 32, ndense = hw3 & 0xFFFFFFFFu;
+        kern = !nblk                       ? kMatchGeneral
+               : 10 * nsmall >= 9 * nblk ? kMatchKey4
+               : 10 * ndense >= 9 * nblk ? kMatchNoFilter
+                                         : kMatchGeneral;
+    }
+    const MatchLaunch match = match_launcher(kern);
+    c->last_kernel = kern;
+    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 32, st));
     if (G > 1) {
         HIP_TRY(hipEventRecord(c->gsync[0], st));
         for (auto s2 : c->gst) HIP_TRY(hipStreamWaitEvent(s2, c->gsync[0], 0));
@@ -405,10 +423,10 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         }
     }
     HIP_TRY(hipGetLastError());
-    if (!out_len && c->key4 < 0 && c->calls++ % kKeyProbe == 0)
-        HIP_TRY(hipMemcpyAsync(c->host_words + 2, c->dev_words + 2, 8, hipMemcpyDeviceToHost, st));
+    if (!out_len && c->kernel == kMatchAuto && c->calls++ % kKeyProbe == 0)
+        HIP_TRY(hipMemcpyAsync(c->host_words + 2, c->dev_words + 2, 16, hipMemcpyDeviceToHost, st));
     if (out_len) {
-        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 24, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 32, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         const uint32_t e = (uint32_t)c->host_words[1];
         if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
@@ -455,8 +473,8 @@ int fcx_debug_emit_bits(fcx_ctx *c, uint32_t bits) {
     return FCX_OK;
 }
 
-// testing only (not in fcx.h): the key width of the last call's match kernel (3 or 4)
-int fcx_debug_match_key(fcx_ctx *c) { return c ? (c->last_key4 ? 4 : 3) : 0; }
+// testing only (not in fcx.h): the last call's match kernel (0 general, 1 4-byte keys, 2 no filter)
+int fcx_debug_match_kernel(fcx_ctx *c) { return c ? c->last_kernel : -1; }
 
 // development only (not in fcx.h): the match kernel alone with experiment bits, for
 // per-phase timing (tools/matchphase.py); the context's scratch is left invalid
@@ -466,8 +484,8 @@ int fcx_debug_match(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint32_t dbg, v
     int r = ensure_scratch(c, n);
     if (r) return r;
     const Layout L = make_layout(n, c->B);
-    (c->key4 == 1 ? launch_match_k4 : launch_match)(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok,
-                                                    (hipStream_t)stream, dbg);
+    match_launcher(c->kernel)(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok, (hipStream_t)stream,
+                              dbg);
     HIP_TRY(hipGetLastError());
     return FCX_OK;
 }

@@ -58,6 +58,17 @@
 #define k_match k_match_k4
 #define launch_match launch_match_k4
 #endif
+// FCX_NOFILTER (fcx_match_nf.hip): the kernel without the repeat sample, the repeat filter and the
+// sparse search, for shards of match-dense blocks (text: every tile takes the bucket search there,
+// so the sampled filter that sends random-data tiles to the sparse search is wasted work, ~0.6 ms
+// per GiB).  Chosen per call like the 4-byte-key unit; the same bytes either way.
+#ifndef FCX_NOFILTER
+#define FCX_NOFILTER 0
+#endif
+#if FCX_NOFILTER
+#define k_match k_match_nf
+#define launch_match launch_match_nf
+#endif
 
 namespace fcx {
 
@@ -760,8 +771,10 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
     __shared__ uint32_t s_nruns;    // image runs counted in the first 2 KiB (pass 1)
     __shared__ uint32_t s_nruns2;   // ... and in the rest (pass 2, only when pass 1 allows run mode)
+#if !FCX_NOFILTER
     __shared__ uint32_t s_smp[kSampleWords];   // repeat sample bitmap
     __shared__ uint32_t s_sample;   // repeat sample: sampled keys whose hash was seen before
+#endif
     __shared__ uint32_t s_events;   // repeat filter: window keys whose hash was seen before
     __shared__ uint32_t s_np;       // sparse search: positions whose hash repeats
     __shared__ uint32_t s_chg[2];
@@ -810,14 +823,20 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         }
     }
     if (tid == 0) {
+#if FCX_NOFILTER
+        s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_chg[0] = 0; s_chg[1] = 0;
+#else
         s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_sample = 0; s_chg[0] = 0; s_chg[1] = 0;
+#endif
         s_events = 0; s_np = 0;
     }
+#if !FCX_NOFILTER
     if (tid < kSampleWords) s_smp[tid] = 0;
     {   // the repeat filter's bitmaps are zeroed here, under the staging loads' latency
         uint4 *r4 = (uint4 *)region;
         for (uint32_t x = tid; x < kFilterWords / 4; x += kMT) r4[x] = make_uint4(0u, 0u, 0u, 0u);
     }
+#endif
     __syncthreads();
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
@@ -842,6 +861,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         uint32_t cnt = (tid == 0 && nload > 0 ? 1u : 0u) + runs_in(tid);
         cnt = wave_sum_u32(cnt);
         if ((tid & 63) == 0) atomicAdd(&s_nruns, cnt);
+#if !FCX_NOFILTER
         {   // repeat sample: the key of every 12th window position into a 2^12-bit bitmap;
             // random data repeats ~32 times in 512 samples, text far more often
             const uint32_t x = kIns * tid;
@@ -854,6 +874,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
             const uint64_t bal = __ballot(rep);
             if ((tid & 63) == 0 && bal) atomicAdd(&s_sample, (uint32_t)__popcll(bal));
         }
+#endif
         __syncthreads();
         if (s_nruns <= kRunTile) {   // (s_nruns is final here: the decision is uniform)
             cnt = 0;
@@ -895,7 +916,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // repeat.  Random data has a few hundred repeats per tile (almost all hash
     // collisions), so the search below visits only the positions whose hash repeats
     // (sparse search); above kSparseEvents repeats the tile takes the bucket search. ----
+#if FCX_NOFILTER
+    if (false) {
+#else
     if (s_sample <= kSampleEvents && !(dbg & 128u)) {
+#endif
     uint32_t *seen = region, *dupm = region + kFilterWords / 2;   // (zeroed with the staging)
     {
         // all 12 "seen" atomics in flight at once (program order keeps a lane's own

@@ -60,11 +60,12 @@ def test_golden_cases_bit_exact(golden, gpu_compress):
     assert not bad, f"GPU output differs from the reference on {bad}"
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4])
+@pytest.mark.parametrize("mode", [1, 2, 4, 5])
 def test_golden_cases_forced_match_mode(golden, gpu_compress, mode):
     """every tile through one evaluation path of k_match (1: hash buckets + run table
-    for the unknowns, 2: run table for whole tiles, 4: every call through the 4-byte-key
-    kernel, whatever the data): the output must not change"""
+    for the unknowns, 2: run table for whole tiles; 4: every call through the 4-byte-key
+    kernel, 5: through the kernel without the repeat filter, whatever the data): the
+    output must not change"""
     bad = []
     for case in _cases(golden):
         if case["in_bytes"] > 1 << 20:
@@ -335,8 +336,8 @@ def test_key4_kernel_vs_oracle(cuda, block):
 
     import torch
 
-    key = mc.lib().fcx_debug_match_key
-    key.argtypes, key.restype = [ctypes.c_void_p], ctypes.c_int
+    kernel = mc.lib().fcx_debug_match_kernel
+    kernel.argtypes, kernel.restype = [ctypes.c_void_p], ctypes.c_int
     cases = [("dna", inputs.generate("dna", 6, 3 << 20)), ("mix", _small_alphabet_mix(5, 3 << 20)),
              ("ragged", bytes(random.Random(7).choice(b"ACGT") for _ in range(100003)))]
     for name, data in cases:
@@ -355,8 +356,39 @@ def test_key4_kernel_vs_oracle(cuda, block):
                     got = mc.write_header(len(data), nb) + d_out[:n].cpu().numpy().tobytes()
                     assert got == want, (name, block, mode, call)
                     if mode == 4:
-                        assert key(ctx._h) == 4
+                        assert kernel(ctx._h) == 1
                     elif name == "dna" and block >= 65536:
-                        assert key(ctx._h) == (3 if call == 0 else 4), (block, call)
+                        assert kernel(ctx._h) == (0 if call == 0 else 1), (block, call)
             finally:
                 ctx.close()
+
+
+@pytest.mark.parametrize("block", [1 << 20, 262144])
+def test_match_dense_kernel_auto(cuda, block):
+    """match-dense shards (text) switch to the kernel without the repeat filter from the
+    second call on, random data stays on the general kernel; the bytes equal the oracle's"""
+    import ctypes
+
+    import torch
+
+    kernel = mc.lib().fcx_debug_match_kernel
+    kernel.argtypes, kernel.restype = [ctypes.c_void_p], ctypes.c_int
+    for name, data, want_kernel in (("text", inputs.generate("text", 3, 3 << 20), 2),
+                                    ("rand", inputs.generate("rand", 4, 3 << 20), 0),
+                                    ("mix", _small_alphabet_mix(9, 2 << 20), None)):
+        want = oracle.compress_file(data, block)
+        d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
+        cap = mc.shard_bound(len(data), block)
+        d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+        nb = (len(data) + block - 1) // block
+        ctx = mc.Context(0, block, len(data))
+        try:
+            for call in range(3):
+                n = ctx.compress_shard(d_in.data_ptr(), len(data), d_out.data_ptr(), cap,
+                                       torch.cuda.current_stream().cuda_stream)
+                got = mc.write_header(len(data), nb) + d_out[:n].cpu().numpy().tobytes()
+                assert got == want, (name, block, call)
+                if want_kernel is not None:
+                    assert kernel(ctx._h) == (0 if call == 0 else want_kernel), (name, block, call)
+        finally:
+            ctx.close()
