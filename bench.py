@@ -345,6 +345,7 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
             else:
                 res["partition"]["source"] = ("--share0" if args.share0_ppm >= 0 else
                                               f"step model at the assumed {args.link_gbps} GB/s link")
+    res["match_kernel"] = ctx.match_kernel() if n else None   # (the timed steps' match stage)
     stats = ctx.stats() if n else {"tokens": 0, "matches": 0, "lazy_evals": 0, "lazy_tiles": 0}
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
@@ -648,10 +649,12 @@ def roofline(res, pmc_leg, pmc):
     alg = n + res["seg_bytes_rank0"]
     achieved = alg / (stages[dom] * 1e-3) / 1e9 if dom else None
     traffic = None
-    key = f"{pmc_leg}:{dom}"
+    # the match stage runs one of k_match's units (fcx_ctx_match_kernel): the kernel name is that unit's
+    kernel = (res.get("match_kernel") or "k_match") if dom == "match" else f"k_{dom}" if dom else None
+    key = f"{pmc_leg}:{kernel[2:]}" if kernel else None
     if pmc_leg and key in pmc:   # PMC passes ran on a whole 1 GiB shard; scale to this rank's launch
         traffic = pmc[key].get("hbm_bytes_per_launch") * n / pmc[key].get("input_bytes", GiB)
-    return {"bound": "hbm", "kernel": f"k_{dom}" if dom else None, "achieved": achieved, "peak": HBM_PEAK_GBS,
+    return {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
             "alg_bytes_per_launch": alg, "kernel_ms": stages.get(dom),
             "note": "achieved = (this rank's input + its compressed segment) / the dominant kernel's average "

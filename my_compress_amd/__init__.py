@@ -73,6 +73,8 @@ def lib():
     L.fcx_ctx_stage.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                 ctypes.POINTER(ctypes.c_float)]
     L.fcx_ctx_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
+    L.fcx_ctx_match_kernel.argtypes = [ctypes.c_void_p]
+    L.fcx_ctx_match_kernel.restype = ctypes.c_int
     L.fcx_compress_stream.argtypes = [ctypes.c_void_p, READ_FN, WRITE_FN, ctypes.c_void_p, ctypes.c_uint64,
                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]
@@ -226,7 +228,8 @@ class Context:
 
     def set_match_mode(self, mode: int):
         """testing: 0 auto, 1 bucket search, 2 run table for whole tiles, 3 the general
-        kernel, 4 the 4-byte-key kernel, 5 the no-filter kernel (same output; fcx.h)"""
+        kernel, 4 the 4-byte-key kernel, 5 the no-filter kernel, 6 the runs kernel (same output;
+        fcx.h)"""
         _check(lib().fcx_ctx_set_match_mode(self._h, mode), "fcx_ctx_set_match_mode")
 
     def set_groups(self, groups: int):
@@ -247,6 +250,12 @@ class Context:
         vals = [ctypes.c_uint64() for _ in range(5)]
         _check(lib().fcx_ctx_stats(self._h, *[ctypes.byref(v) for v in vals]), "fcx_ctx_stats")
         return dict(zip(["tokens", "matches", "lazy_evals", "lazy_tiles", "tiles"], [v.value for v in vals]))
+
+    MATCH_KERNELS = ("k_match", "k_match_k4", "k_match_nf", "k_match_runs")
+
+    def match_kernel(self) -> str:
+        """the kernel the last compress_shard call's match stage ran (fcx_ctx_match_kernel)"""
+        return self.MATCH_KERNELS[lib().fcx_ctx_match_kernel(self._h)]
 
 
 class DContext:

@@ -20,6 +20,8 @@ void launch_match_k4(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *
                      uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_match_nf(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
                      uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
+void launch_match_runs(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                       uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -88,12 +90,14 @@ void set_last_error(const std::string &m) { g_err = m; }
 
 constexpr uint64_t kKeyProbe = 16;   // calls without a length read per read of the block-kind counts
 
-// the match kernel's translation units (fcx_match.hip, fcx_match_k4.hip, fcx_match_nf.hip)
-enum MatchKernel : int { kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2 };
+// the match kernel's translation units (fcx_match.hip, fcx_match_k4.hip, fcx_match_nf.hip, fcx_match_runs.hip)
+enum MatchKernel : int { kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2, kMatchRuns = 3 };
 using MatchLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64_t *, uint64_t *, uint64_t *,
                              uint32_t *, uint32_t *, hipStream_t, uint32_t);
 static MatchLaunch match_launcher(int k) {
-    return k == kMatchKey4 ? launch_match_k4 : k == kMatchNoFilter ? launch_match_nf : launch_match;
+    return k == kMatchKey4 ? launch_match_k4 : k == kMatchNoFilter ? launch_match_nf
+                                             : k == kMatchRuns    ? launch_match_runs
+                                                                  : launch_match;
 }
 
 struct fcx_ctx {
@@ -120,7 +124,8 @@ struct fcx_ctx {
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
     uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits, [2] = small-alphabet
-                                       // blocks | blocks << 32, [3] = match-dense blocks (k_tree, u32)
+                                       // blocks | blocks << 32, [3] = match-dense | long-match blocks << 32
+                                       // (k_tree)
     uint64_t *host_words = nullptr;    // pinned mirror ([2..3]: refreshed by the length reads, and by an
                                        // asynchronous copy every kKeyProbe-th call without one)
     uint64_t calls = 0;
@@ -298,11 +303,15 @@ int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
 
 int fcx_ctx_set_match_mode(fcx_ctx *c, int mode) {
     if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
-    if (mode < 0 || mode > 5)
+    if (mode < 0 || mode > 6)
         return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search), 2 (run table), "
-                                 "3 (general kernel), 4 (4-byte-key kernel) or 5 (no-filter kernel)");
+                                 "3 (general kernel), 4 (4-byte-key kernel), 5 (no-filter kernel) or 6 (runs kernel)");
     c->match_mode = mode == 1 ? 4u | 128u : mode == 2 ? 8u : 0u;   // k_match dbg bits: all keep the output exact
-    c->kernel = mode == 0 ? kMatchAuto : mode == 4 ? kMatchKey4 : mode == 5 ? kMatchNoFilter : kMatchGeneral;
+    c->kernel = mode == 0   ? kMatchAuto
+                : mode == 4 ? kMatchKey4
+                : mode == 5 ? kMatchNoFilter
+                : mode == 6 ? kMatchRuns
+                            : kMatchGeneral;
     return FCX_OK;
 }
 
@@ -362,16 +371,18 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
 
     // match kernel: when >= 90 % of a recent call's blocks had small alphabets (dense 3-byte keys:
     // 'ACGT' data) the 4-byte-key one, else when >= 90 % were match-dense (text) the one without the
-    // repeat filter, else the general one; all give the same bytes.  (host_words[2..3]
+    // repeat filter, else when >= 90 % were long-match blocks (runs, zeros) the one with the run-mode
+    // walk inlined, else the general one; all give the same bytes.  (host_words[2..3]
     // may be landing from an earlier call's copy: any value is a valid choice)
     int kern = c->kernel;
     if (kern == kMatchAuto) {
         const uint64_t hw2 = __atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);
         const uint64_t hw3 = __atomic_load_n(&c->host_words[3], __ATOMIC_RELAXED);
-        const uint64_t nsmall = hw2 & 0xFFFFFFFFu, nblk = hw2 >> 32, ndense = hw3 & 0xFFFFFFFFu;
+        const uint64_t nsmall = hw2 & 0xFFFFFFFFu, nblk = hw2 >> 32, ndense = hw3 & 0xFFFFFFFFu, nlong = hw3 >> 32;
         kern = !nblk                       ? kMatchGeneral
                : 10 * nsmall >= 9 * nblk ? kMatchKey4
                : 10 * ndense >= 9 * nblk ? kMatchNoFilter
+               : 10 * nlong >= 9 * nblk  ? kMatchRuns
                                          : kMatchGeneral;
     }
     const MatchLaunch match = match_launcher(kern);
@@ -473,8 +484,7 @@ int fcx_debug_emit_bits(fcx_ctx *c, uint32_t bits) {
     return FCX_OK;
 }
 
-// testing only (not in fcx.h): the last call's match kernel (0 general, 1 4-byte keys, 2 no filter)
-int fcx_debug_match_kernel(fcx_ctx *c) { return c ? c->last_kernel : -1; }
+int fcx_ctx_match_kernel(fcx_ctx *c) { return c ? c->last_kernel : -1; }
 
 // development only (not in fcx.h): the match kernel alone with experiment bits, for
 // per-phase timing (tools/matchphase.py); the context's scratch is left invalid

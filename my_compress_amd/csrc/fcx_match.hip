@@ -69,6 +69,20 @@
 #define k_match k_match_nf
 #define launch_match launch_match_nf
 #endif
+// FCX_RUNS (fcx_match_runs.hip): the kernel with the run-mode walk inlined, for shards of long-match
+// blocks (runs, zeros).  Out of line, the walk saves callee-saved VGPRs to scratch on every run-mode
+// tile (16 KB per tile, written to HBM); inlined, the other tile modes' register allocation moves,
+// which only this unit's shards pay.
+#ifndef FCX_RUNS
+#define FCX_RUNS 0
+#endif
+#if FCX_RUNS
+#define k_match k_match_runs
+#define launch_match launch_match_runs
+#define FCX_RMODE_CALL __forceinline__
+#else
+#define FCX_RMODE_CALL __noinline__
+#endif
 
 namespace fcx {
 
@@ -347,7 +361,7 @@ __device__ inline uint32_t rm_stepat(FCX_LDS uint32_t *region, uint32_t x, uint3
     return sv;
 }
 
-__device__ __noinline__ void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32_t *s_ex, FCX_LDS uint32_t *s_unknown,
+__device__ FCX_RMODE_CALL void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32_t *s_ex, FCX_LDS uint32_t *s_unknown,
                                         uint32_t q0, uint32_t nt, uint32_t ilen, uint32_t w0, uint32_t t0, uint64_t *mbw,
                                         uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t *mt, uint32_t dbg) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);   // walks: wave-uniform, scalar

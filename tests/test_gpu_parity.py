@@ -60,12 +60,12 @@ def test_golden_cases_bit_exact(golden, gpu_compress):
     assert not bad, f"GPU output differs from the reference on {bad}"
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4, 5])
+@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6])
 def test_golden_cases_forced_match_mode(golden, gpu_compress, mode):
     """every tile through one evaluation path of k_match (1: hash buckets + run table
     for the unknowns, 2: run table for whole tiles; 4: every call through the 4-byte-key
-    kernel, 5: through the kernel without the repeat filter, whatever the data): the
-    output must not change"""
+    kernel, 5: through the kernel without the repeat filter, 6: through the kernel with the
+    run-mode walk inlined, whatever the data): the output must not change"""
     bad = []
     for case in _cases(golden):
         if case["in_bytes"] > 1 << 20:
@@ -332,12 +332,9 @@ def test_key4_kernel_vs_oracle(cuda, block):
     context from its previous call (mode 0: 'ACGT' data switches from the second call on),
     against the oracle on dna, mixed small-alphabet / text / random / periodic data and a
     ragged tail"""
-    import ctypes
-
     import torch
 
-    kernel = mc.lib().fcx_debug_match_kernel
-    kernel.argtypes, kernel.restype = [ctypes.c_void_p], ctypes.c_int
+    kernel = mc.lib().fcx_ctx_match_kernel
     cases = [("dna", inputs.generate("dna", 6, 3 << 20)), ("mix", _small_alphabet_mix(5, 3 << 20)),
              ("ragged", bytes(random.Random(7).choice(b"ACGT") for _ in range(100003)))]
     for name, data in cases:
@@ -366,15 +363,15 @@ def test_key4_kernel_vs_oracle(cuda, block):
 @pytest.mark.parametrize("block", [1 << 20, 262144])
 def test_match_dense_kernel_auto(cuda, block):
     """match-dense shards (text) switch to the kernel without the repeat filter from the
-    second call on, random data stays on the general kernel; the bytes equal the oracle's"""
-    import ctypes
-
+    second call on, long-match shards (runs, zeros) to the runs kernel, random data stays on
+    the general kernel; the bytes equal the oracle's"""
     import torch
 
-    kernel = mc.lib().fcx_debug_match_kernel
-    kernel.argtypes, kernel.restype = [ctypes.c_void_p], ctypes.c_int
+    kernel = mc.lib().fcx_ctx_match_kernel
     for name, data, want_kernel in (("text", inputs.generate("text", 3, 3 << 20), 2),
                                     ("rand", inputs.generate("rand", 4, 3 << 20), 0),
+                                    ("runs", inputs.generate("runs", 5, 3 << 20), 3),
+                                    ("zeros", bytes(3 << 20), 3),
                                     ("mix", _small_alphabet_mix(9, 2 << 20), None)):
         want = oracle.compress_file(data, block)
         d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
