@@ -132,12 +132,13 @@ int fcx_ctx_set_profiling(fcx_ctx *ctx, int enable);
  * repeat, else bucket search), 1 bucket search for every tile (unknown positions
  * via the run table / the stitch), 2 run table for whole tiles, 3 the general kernel for
  * every call, 4 the 4-byte-key kernel for every call, 5 the kernel without the repeat
- * filter for every call, 6 the kernel with the run-mode walk inlined for every call
- * (auto: the 4-byte-key kernel when >= 90 % of the blocks of a recent call had small
- * alphabets, e.g. 'ACGT' data, else the no-filter kernel when >= 90 % were match-dense,
- * e.g. text, else the runs kernel when >= 90 % had long matches, e.g. runs or zeros, else
- * the general one; the recent call is the one before when its length was read back, else
- * the last of every 16th call).  The output is identical in every mode; only the speed
+ * filter for every call, 6 the kernel with the run-mode walk inlined for every call, 7
+ * the kernel without the bucket search for every call (auto: the 4-byte-key kernel when
+ * >= 90 % of the blocks of a recent call had small alphabets, e.g. 'ACGT' data, else the
+ * no-filter kernel when >= 90 % were match-dense, e.g. text, else the runs kernel when
+ * >= 90 % had long matches, e.g. runs or zeros, else the sparse kernel when >= 90 % had
+ * few matches, e.g. random data, else the general one; the recent call is the one before
+ * when its length was read back, else the last of every 16th call).  The output is identical in every mode; only the speed
  * differs. */
 int fcx_ctx_set_match_mode(fcx_ctx *ctx, int mode);
 /* Pipelined launch: fcx_compress_shard splits the shard's blocks into `groups` groups
@@ -155,7 +156,8 @@ int fcx_ctx_stats(fcx_ctx *ctx, uint64_t *tokens, uint64_t *matches, uint64_t *l
                   uint64_t *lazy_tiles, uint64_t *tiles);
 /* The match kernel the last fcx_compress_shard call ran: 0 general, 1 4-byte keys (small
  * alphabets), 2 without the repeat filter (match-dense data), 3 run-mode walk inlined
- * (long matches); -1 for a NULL ctx (fcx_ctx_set_match_mode). */
+ * (long matches), 4 without the bucket search (few matches); -1 for a NULL ctx
+ * (fcx_ctx_set_match_mode). */
 int fcx_ctx_match_kernel(fcx_ctx *ctx);
 
 /* ---- GPU decoder ------------------------------------------------------------ */

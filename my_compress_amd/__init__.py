@@ -228,8 +228,8 @@ class Context:
 
     def set_match_mode(self, mode: int):
         """testing: 0 auto, 1 bucket search, 2 run table for whole tiles, 3 the general
-        kernel, 4 the 4-byte-key kernel, 5 the no-filter kernel, 6 the runs kernel (same output;
-        fcx.h)"""
+        kernel, 4 the 4-byte-key kernel, 5 the no-filter kernel, 6 the runs kernel, 7 the sparse
+        kernel (same output; fcx.h)"""
         _check(lib().fcx_ctx_set_match_mode(self._h, mode), "fcx_ctx_set_match_mode")
 
     def set_groups(self, groups: int):
@@ -251,7 +251,7 @@ class Context:
         _check(lib().fcx_ctx_stats(self._h, *[ctypes.byref(v) for v in vals]), "fcx_ctx_stats")
         return dict(zip(["tokens", "matches", "lazy_evals", "lazy_tiles", "tiles"], [v.value for v in vals]))
 
-    MATCH_KERNELS = ("k_match", "k_match_k4", "k_match_nf", "k_match_runs")
+    MATCH_KERNELS = ("k_match", "k_match_k4", "k_match_nf", "k_match_runs", "k_match_sparse")
 
     def match_kernel(self) -> str:
         """the kernel the last compress_shard call's match stage ran (fcx_ctx_match_kernel)"""

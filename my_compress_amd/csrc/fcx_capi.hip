@@ -22,6 +22,8 @@ void launch_match_nf(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *
                      uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_match_runs(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
                        uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
+void launch_match_sparse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                         uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -90,13 +92,16 @@ void set_last_error(const std::string &m) { g_err = m; }
 
 constexpr uint64_t kKeyProbe = 16;   // calls without a length read per read of the block-kind counts
 
-// the match kernel's translation units (fcx_match.hip, fcx_match_k4.hip, fcx_match_nf.hip, fcx_match_runs.hip)
-enum MatchKernel : int { kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2, kMatchRuns = 3 };
+// the match kernel's translation units (fcx_match.hip and the fcx_match_<kind>.hip units that include it)
+enum MatchKernel : int {
+    kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2, kMatchRuns = 3, kMatchSparse = 4
+};
 using MatchLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64_t *, uint64_t *, uint64_t *,
                              uint32_t *, uint32_t *, hipStream_t, uint32_t);
 static MatchLaunch match_launcher(int k) {
     return k == kMatchKey4 ? launch_match_k4 : k == kMatchNoFilter ? launch_match_nf
                                              : k == kMatchRuns    ? launch_match_runs
+                                             : k == kMatchSparse  ? launch_match_sparse
                                                                   : launch_match;
 }
 
@@ -124,9 +129,9 @@ struct fcx_ctx {
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
     uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits, [2] = small-alphabet
-                                       // blocks | blocks << 32, [3] = match-dense | long-match blocks << 32
-                                       // (k_tree)
-    uint64_t *host_words = nullptr;    // pinned mirror ([2..3]: refreshed by the length reads, and by an
+                                       // blocks | blocks << 32, [3] = match-dense | long-match blocks << 32,
+                                       // [4] = few-match blocks (k_tree)
+    uint64_t *host_words = nullptr;    // pinned mirror ([2..4]: refreshed by the length reads, and by an
                                        // asynchronous copy every kKeyProbe-th call without one)
     uint64_t calls = 0;
     int last_kernel = kMatchGeneral;   // the last call's match kernel
@@ -287,7 +292,7 @@ int fcx_ctx_read_out_len(fcx_ctx *c, uint64_t *out_len) {
     if (!c || !out_len) return fail(FCX_ERR_ARG, "fcx_ctx_read_out_len: NULL");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 32, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 40, hipMemcpyDeviceToHost));
     const uint32_t e = (uint32_t)c->host_words[1];
     if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
     if (e) return fail(FCX_ERR_INTERNAL, "device invariant violated (error bits " + std::to_string(e) + ")");
@@ -303,14 +308,15 @@ int fcx_ctx_set_profiling(fcx_ctx *c, int enable) {
 
 int fcx_ctx_set_match_mode(fcx_ctx *c, int mode) {
     if (!c) return fail(FCX_ERR_ARG, "NULL ctx");
-    if (mode < 0 || mode > 6)
-        return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search), 2 (run table), "
-                                 "3 (general kernel), 4 (4-byte-key kernel), 5 (no-filter kernel) or 6 (runs kernel)");
+    if (mode < 0 || mode > 7)
+        return fail(FCX_ERR_ARG, "match mode must be 0 (auto), 1 (bucket search), 2 (run table), 3 (general kernel), "
+                                 "4 (4-byte-key kernel), 5 (no-filter kernel), 6 (runs kernel) or 7 (sparse kernel)");
     c->match_mode = mode == 1 ? 4u | 128u : mode == 2 ? 8u : 0u;   // k_match dbg bits: all keep the output exact
     c->kernel = mode == 0   ? kMatchAuto
                 : mode == 4 ? kMatchKey4
                 : mode == 5 ? kMatchNoFilter
                 : mode == 6 ? kMatchRuns
+                : mode == 7 ? kMatchSparse
                             : kMatchGeneral;
     return FCX_OK;
 }
@@ -372,22 +378,25 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     // match kernel: when >= 90 % of a recent call's blocks had small alphabets (dense 3-byte keys:
     // 'ACGT' data) the 4-byte-key one, else when >= 90 % were match-dense (text) the one without the
     // repeat filter, else when >= 90 % were long-match blocks (runs, zeros) the one with the run-mode
-    // walk inlined, else the general one; all give the same bytes.  (host_words[2..3]
-    // may be landing from an earlier call's copy: any value is a valid choice)
+    // walk inlined, else when >= 90 % were few-match blocks (random data) the one without the bucket
+    // search, else the general one; all give the same bytes.  (host_words[2..4] may be
+    // landing from an earlier call's copy: any value is a valid choice)
     int kern = c->kernel;
     if (kern == kMatchAuto) {
         const uint64_t hw2 = __atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);
         const uint64_t hw3 = __atomic_load_n(&c->host_words[3], __ATOMIC_RELAXED);
+        const uint64_t nfew = __atomic_load_n(&c->host_words[4], __ATOMIC_RELAXED) & 0xFFFFFFFFu;
         const uint64_t nsmall = hw2 & 0xFFFFFFFFu, nblk = hw2 >> 32, ndense = hw3 & 0xFFFFFFFFu, nlong = hw3 >> 32;
         kern = !nblk                       ? kMatchGeneral
                : 10 * nsmall >= 9 * nblk ? kMatchKey4
                : 10 * ndense >= 9 * nblk ? kMatchNoFilter
                : 10 * nlong >= 9 * nblk  ? kMatchRuns
+               : 10 * nfew >= 9 * nblk   ? kMatchSparse
                                          : kMatchGeneral;
     }
     const MatchLaunch match = match_launcher(kern);
     c->last_kernel = kern;
-    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 32, st));
+    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 40, st));
     if (G > 1) {
         HIP_TRY(hipEventRecord(c->gsync[0], st));
         for (auto s2 : c->gst) HIP_TRY(hipStreamWaitEvent(s2, c->gsync[0], 0));
@@ -435,9 +444,9 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     }
     HIP_TRY(hipGetLastError());
     if (!out_len && c->kernel == kMatchAuto && c->calls++ % kKeyProbe == 0)
-        HIP_TRY(hipMemcpyAsync(c->host_words + 2, c->dev_words + 2, 16, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->host_words + 2, c->dev_words + 2, 24, hipMemcpyDeviceToHost, st));
     if (out_len) {
-        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 32, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 40, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         const uint32_t e = (uint32_t)c->host_words[1];
         if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");

@@ -76,6 +76,18 @@
 #ifndef FCX_RUNS
 #define FCX_RUNS 0
 #endif
+// FCX_SPARSE (fcx_match_sparse.hip): the kernel without the bucket search, for shards of few-match
+// blocks (random data: every tile takes the sparse search).  A tile the repeat filter does not send
+// to the sparse search takes the whole-tile run-table mode instead (exact for any tile, slow where
+// the runs overflow the table: fcx_ctx_set_match_mode 2); the search phases' registers no longer
+// weigh on the sparse path.
+#ifndef FCX_SPARSE
+#define FCX_SPARSE 0
+#endif
+#if FCX_SPARSE
+#define k_match k_match_sparse
+#define launch_match launch_match_sparse
+#endif
 #if FCX_RUNS
 #define k_match k_match_runs
 #define launch_match launch_match_runs
@@ -778,9 +790,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
     // search, [step (u16 x 4096) | parse scratch] after it
     __shared__ __attribute__((aligned(16))) uint32_t region[kRegionWords];
+#if !FCX_SPARSE
     uint32_t *hw = region;                                  // packed u16 bucket counters, then starts
     uint16_t *h16 = (uint16_t *)region;
     uint16_t *ent = (uint16_t *)(region + kHeadWords);     // window entries, bucket-sorted
+#endif
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
     __shared__ uint32_t s_nruns;    // image runs counted in the first 2 KiB (pass 1)
@@ -899,7 +913,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         }
     }
     const uint32_t nruns_img = s_nruns + s_nruns2;   // s_nruns2 = 0 unless pass 2 ran (then after its barrier)
+#if FCX_SPARSE
+    bool rmode = (nruns_img <= kRunTile && !(dbg & 4u)) || (dbg & 8u);   // (set below for non-sparse tiles)
+#else
     const bool rmode = (nruns_img <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
+#endif
     if (dbg & 16u) return;   // timing: staging + run count only
 
     // this lane's 12 consecutive window positions 12 tid .. 12 tid + 11 take their keys from
@@ -971,6 +989,14 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                       mbits + (uint64_t)b * L.wpb + (t0 >> 6), q0, npos, ins_end, w0, blen, t1 - t0, dbg);
         __syncthreads();
         if (dbg & 32u) return;
+#if FCX_SPARSE
+    } else {   // not sparse: the whole-tile run-table mode, as for run-mode tiles
+        rmode = true;
+        for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
+        if (tid == 0) s_unknown = 1;
+        __syncthreads();
+    }
+#else
     } else {
     for (uint32_t x = tid; x < kHeadWords; x += kMT) hw[x] = 0;
     __syncthreads();
@@ -1319,6 +1345,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     __syncthreads();
     }   // bucket search
+#endif
     }   // filter: sparse or bucket search
 
     // ---- 3b. dense windows: exact matches of the unknown positions over the run table ----

@@ -60,12 +60,13 @@ def test_golden_cases_bit_exact(golden, gpu_compress):
     assert not bad, f"GPU output differs from the reference on {bad}"
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6])
+@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7])
 def test_golden_cases_forced_match_mode(golden, gpu_compress, mode):
     """every tile through one evaluation path of k_match (1: hash buckets + run table
     for the unknowns, 2: run table for whole tiles; 4: every call through the 4-byte-key
     kernel, 5: through the kernel without the repeat filter, 6: through the kernel with the
-    run-mode walk inlined, whatever the data): the output must not change"""
+    run-mode walk inlined, 7: through the kernel without the bucket search, whatever the
+    data): the output must not change"""
     bad = []
     for case in _cases(golden):
         if case["in_bytes"] > 1 << 20:
@@ -363,13 +364,13 @@ def test_key4_kernel_vs_oracle(cuda, block):
 @pytest.mark.parametrize("block", [1 << 20, 262144])
 def test_match_dense_kernel_auto(cuda, block):
     """match-dense shards (text) switch to the kernel without the repeat filter from the
-    second call on, long-match shards (runs, zeros) to the runs kernel, random data stays on
-    the general kernel; the bytes equal the oracle's"""
+    second call on, long-match shards (runs, zeros) to the runs kernel, random data to the
+    kernel without the bucket search; the bytes equal the oracle's"""
     import torch
 
     kernel = mc.lib().fcx_ctx_match_kernel
     for name, data, want_kernel in (("text", inputs.generate("text", 3, 3 << 20), 2),
-                                    ("rand", inputs.generate("rand", 4, 3 << 20), 0),
+                                    ("rand", inputs.generate("rand", 4, 3 << 20), 4),
                                     ("runs", inputs.generate("runs", 5, 3 << 20), 3),
                                     ("zeros", bytes(3 << 20), 3),
                                     ("mix", _small_alphabet_mix(9, 2 << 20), None)):
