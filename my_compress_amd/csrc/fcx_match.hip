@@ -102,7 +102,11 @@ constexpr uint32_t kWinPos = kHalo + 1 + kTile;      // 6144 window positions pe
 constexpr uint32_t kMT = kMatchThreads;              // 512
 constexpr uint32_t kSeg = kTile / kMT;               // 8 positions per lane in the parse
 constexpr uint32_t kQPL = kTile / kMT;               // 8 queries per lane
+#if defined(FCX_UNIT_ILP)
+constexpr uint32_t kIlp = FCX_UNIT_ILP;   // a unit's own width (fcx_match_nf.hip)
+#else
 constexpr uint32_t kIlp = 4;                         // interleaved chain walks per lane
+#endif
 constexpr uint32_t kWaves = kMT / 64;
 constexpr uint32_t kHeadWords = (1u << kHashBits) / 2 + 4;                 // u16 counters + sentinel
 constexpr uint32_t kEntWords = kWinPos / 2;                                 // u16 entries

@@ -53,7 +53,8 @@ def main():
         torch.cuda.synchronize()
         dt = (time.time() - t) / a.reps
         got = ctx.read_out_len()
-        print(f"groups {G}: {dt * 1e3:.3f} ms  {n / dt / 1e9:.2f} GB/s  out={got} ratio={got / n:.4f}", flush=True)
+        print(f"groups {G}: {dt * 1e3:.3f} ms  {n / dt / 1e9:.2f} GB/s  out={got} ratio={got / n:.4f}"
+              f"  {ctx.match_kernel()}", flush=True)
         ctx.set_profiling(True)
         ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)
         print("   " + "  ".join(f"{name} {ms:.3f}" for name, ms in ctx.stage_times()))
