@@ -76,17 +76,22 @@
 #ifndef FCX_RUNS
 #define FCX_RUNS 0
 #endif
-// FCX_SPARSE (fcx_match_sparse.hip): the kernel without the bucket search, for shards of few-match
-// blocks (random data: every tile takes the sparse search).  A tile the repeat filter does not send
-// to the sparse search takes the whole-tile run-table mode instead (exact for any tile, slow where
-// the runs overflow the table: fcx_ctx_set_match_mode 2); the search phases' registers no longer
-// weigh on the sparse path.
+// FCX_SPARSE (fcx_match_sparse.hip): the kernel without the bucket search, the repeat sample and the
+// run count, for shards of few-match blocks (random data: every tile takes the sparse search).  Every
+// tile runs the repeat filter; a tile it does not send to the sparse search takes the whole-tile
+// run-table mode instead (exact for any tile, slow where the runs overflow the table:
+// fcx_ctx_set_match_mode 2).  Rand k_match 2.64 -> 2.45 ms per GiB.
 #ifndef FCX_SPARSE
 #define FCX_SPARSE 0
 #endif
 #if FCX_SPARSE
 #define k_match k_match_sparse
 #define launch_match launch_match_sparse
+#endif
+#if !FCX_NOFILTER && !FCX_SPARSE
+#define FCX_SAMPLE 1   // the repeat sample decides whether the filter runs
+#else
+#define FCX_SAMPLE 0
 #endif
 #if FCX_RUNS
 #define k_match k_match_runs
@@ -801,9 +806,11 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 #endif
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
+#if !FCX_SPARSE
     __shared__ uint32_t s_nruns;    // image runs counted in the first 2 KiB (pass 1)
     __shared__ uint32_t s_nruns2;   // ... and in the rest (pass 2, only when pass 1 allows run mode)
-#if !FCX_NOFILTER
+#endif
+#if FCX_SAMPLE
     __shared__ uint32_t s_smp[kSampleWords];   // repeat sample bitmap
     __shared__ uint32_t s_sample;   // repeat sample: sampled keys whose hash was seen before
 #endif
@@ -855,15 +862,19 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         }
     }
     if (tid == 0) {
-#if FCX_NOFILTER
+#if FCX_SPARSE
+        s_unknown = 0; s_match = 0; s_chg[0] = 0; s_chg[1] = 0;
+#elif !FCX_SAMPLE
         s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_chg[0] = 0; s_chg[1] = 0;
 #else
         s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_sample = 0; s_chg[0] = 0; s_chg[1] = 0;
 #endif
         s_events = 0; s_np = 0;
     }
-#if !FCX_NOFILTER
+#if FCX_SAMPLE
     if (tid < kSampleWords) s_smp[tid] = 0;
+#endif
+#if !FCX_NOFILTER
     {   // the repeat filter's bitmaps are zeroed here, under the staging loads' latency
         uint4 *r4 = (uint4 *)region;
         for (uint32_t x = tid; x < kFilterWords / 4; x += kMT) r4[x] = make_uint4(0u, 0u, 0u, 0u);
@@ -876,6 +887,9 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
     // ---- 1b. run count of the image: a tile of long runs (zeros, runs) skips the
     // bucket search and takes every match from the run table (dense_phase) ----
+#if FCX_SPARSE
+    const uint32_t nruns_img = kRunTile + 1;   // (no run mode up front: it is the non-sparse tiles' path)
+#else
     {
         // per dword: bytes differing from their predecessor (byte 0 of the image counts
         // once).  The first 2 KiB decide most tiles: more than kRunTile runs there
@@ -893,7 +907,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         uint32_t cnt = (tid == 0 && nload > 0 ? 1u : 0u) + runs_in(tid);
         cnt = wave_sum_u32(cnt);
         if ((tid & 63) == 0) atomicAdd(&s_nruns, cnt);
-#if !FCX_NOFILTER
+#if FCX_SAMPLE
         {   // repeat sample: the key of every 12th window position into a 2^12-bit bitmap;
             // random data repeats ~32 times in 512 samples, text far more often
             const uint32_t x = kIns * tid;
@@ -917,6 +931,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         }
     }
     const uint32_t nruns_img = s_nruns + s_nruns2;   // s_nruns2 = 0 unless pass 2 ran (then after its barrier)
+#endif
 #if FCX_SPARSE
     bool rmode = (nruns_img <= kRunTile && !(dbg & 4u)) || (dbg & 8u);   // (set below for non-sparse tiles)
 #else
@@ -954,6 +969,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // (sparse search); above kSparseEvents repeats the tile takes the bucket search. ----
 #if FCX_NOFILTER
     if (false) {
+#elif !FCX_SAMPLE
+    if (!(dbg & 128u)) {
 #else
     if (s_sample <= kSampleEvents && !(dbg & 128u)) {
 #endif
