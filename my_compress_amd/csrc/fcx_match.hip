@@ -80,13 +80,19 @@
 // run count, for shards of few-match blocks (random data: every tile takes the sparse search).  Every
 // tile runs the repeat filter; a tile it does not send to the sparse search takes the whole-tile
 // run-table mode instead (exact for any tile, slow where the runs overflow the table:
-// fcx_ctx_set_match_mode 2).  Rand k_match 2.64 -> 2.45 ms per GiB.
+// fcx_ctx_set_match_mode 2); the sparse search is inlined.  Rand k_match 2.64 -> 2.31 ms per GiB
+// (DESIGN.md §4).
 #ifndef FCX_SPARSE
 #define FCX_SPARSE 0
 #endif
 #if FCX_SPARSE
 #define k_match k_match_sparse
 #define launch_match launch_match_sparse
+#endif
+#if FCX_SPARSE   // (the sparse search inline in its own unit: rand k_match 2.43 -> 2.31 ms per GiB)
+#define FCX_SPARSE_CALL __forceinline__
+#else
+#define FCX_SPARSE_CALL __noinline__
 #endif
 #if !FCX_NOFILTER && !FCX_SPARSE
 #define FCX_SAMPLE 1   // the repeat sample decides whether the filter runs
@@ -537,7 +543,7 @@ __device__ inline void scan_candidate(const uint32_t *sdw, uint32_t xe, uint32_t
 // Writes step (LDS), m and the tile's mbits words.  Kept out of line: its registers do
 // not weigh on the bucket search.
 template <bool kDev>
-__device__ __noinline__ void sparse_search(const uint32_t *sdw, uint32_t *region, uint32_t kw0, uint32_t kw1,
+__device__ FCX_SPARSE_CALL void sparse_search(const uint32_t *sdw, uint32_t *region, uint32_t kw0, uint32_t kw1,
                                            uint32_t kw2, uint32_t kw3, uint32_t *s_red,
                                            uint32_t *s_np, uint32_t *s_unknown, uint32_t *s_match, uint32_t *mrow,
                                            uint64_t *mbw, uint32_t q0, uint32_t npos, uint32_t ins_end, uint32_t w0,
