@@ -58,10 +58,11 @@
 #define k_match k_match_k4
 #define launch_match launch_match_k4
 #endif
-// FCX_NOFILTER (fcx_match_nf.hip): the kernel without the repeat sample, the repeat filter and the
-// sparse search, for shards of match-dense blocks (text: every tile takes the bucket search there,
-// so the sampled filter that sends random-data tiles to the sparse search is wasted work, ~0.6 ms
-// per GiB).  Chosen per call like the 4-byte-key unit; the same bytes either way.
+// FCX_NOFILTER (fcx_match_nf.hip): the kernel without the repeat sample, the repeat filter, the
+// sparse search and the run count, for shards of match-dense blocks (text: every tile takes the
+// bucket search there, so the sampled filter that sends random-data tiles to the sparse search and
+// the run count that sends long-run tiles to the run mode are wasted work, ~0.8 ms per GiB).
+// Chosen per call like the 4-byte-key unit; the same bytes either way.
 #ifndef FCX_NOFILTER
 #define FCX_NOFILTER 0
 #endif
@@ -812,7 +813,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 #endif
     __shared__ uint32_t s_unknown;
     __shared__ uint32_t s_match;    // some position of the tile has a match (else the chain is every position)
-#if !FCX_SPARSE
+#if !FCX_SPARSE && !FCX_NOFILTER
     __shared__ uint32_t s_nruns;    // image runs counted in the first 2 KiB (pass 1)
     __shared__ uint32_t s_nruns2;   // ... and in the rest (pass 2, only when pass 1 allows run mode)
 #endif
@@ -868,10 +869,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         }
     }
     if (tid == 0) {
-#if FCX_SPARSE
+#if FCX_SPARSE || FCX_NOFILTER
         s_unknown = 0; s_match = 0; s_chg[0] = 0; s_chg[1] = 0;
-#elif !FCX_SAMPLE
-        s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_chg[0] = 0; s_chg[1] = 0;
 #else
         s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_sample = 0; s_chg[0] = 0; s_chg[1] = 0;
 #endif
@@ -893,8 +892,10 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 
     // ---- 1b. run count of the image: a tile of long runs (zeros, runs) skips the
     // bucket search and takes every match from the run table (dense_phase) ----
-#if FCX_SPARSE
-    const uint32_t nruns_img = kRunTile + 1;   // (no run mode up front: it is the non-sparse tiles' path)
+#if FCX_SPARSE || FCX_NOFILTER
+    // (no run count: run mode is the sparse unit's path for non-sparse tiles; the no-filter unit
+    // takes the bucket search for every tile, exact for any tile through the run table / stitch)
+    const uint32_t nruns_img = kRunTile + 1;
 #else
     {
         // per dword: bytes differing from their predecessor (byte 0 of the image counts
