@@ -54,10 +54,6 @@
 #ifndef FCX_KEY4
 #define FCX_KEY4 0
 #endif
-#if FCX_KEY4
-#define k_match k_match_k4
-#define launch_match launch_match_k4
-#endif
 // FCX_NOFILTER (fcx_match_nf.hip): the kernel without the repeat sample, the repeat filter, the
 // sparse search and the run count, for shards of match-dense blocks (text: every tile takes the
 // bucket search there, so the sampled filter that sends random-data tiles to the sparse search and
@@ -65,10 +61,6 @@
 // Chosen per call like the 4-byte-key unit; the same bytes either way.
 #ifndef FCX_NOFILTER
 #define FCX_NOFILTER 0
-#endif
-#if FCX_NOFILTER
-#define k_match k_match_nf
-#define launch_match launch_match_nf
 #endif
 // FCX_RUNS (fcx_match_runs.hip): the kernel with the run-mode walk inlined, for shards of long-match
 // blocks (runs, zeros).  Out of line, the walk saves callee-saved VGPRs to scratch on every run-mode
@@ -86,10 +78,6 @@
 #ifndef FCX_SPARSE
 #define FCX_SPARSE 0
 #endif
-#if FCX_SPARSE
-#define k_match k_match_sparse
-#define launch_match launch_match_sparse
-#endif
 #if FCX_SPARSE   // (the sparse search inline in its own unit: rand k_match 2.43 -> 2.31 ms per GiB)
 #define FCX_SPARSE_CALL __forceinline__
 #else
@@ -100,9 +88,22 @@
 #else
 #define FCX_SAMPLE 0
 #endif
-#if FCX_RUNS
+// the unit's kernel and launcher names (a unit may combine switches: the 4-byte-key unit also drops
+// the filter and the run count)
+#if FCX_KEY4
+#define k_match k_match_k4
+#define launch_match launch_match_k4
+#elif FCX_NOFILTER
+#define k_match k_match_nf
+#define launch_match launch_match_nf
+#elif FCX_SPARSE
+#define k_match k_match_sparse
+#define launch_match launch_match_sparse
+#elif FCX_RUNS
 #define k_match k_match_runs
 #define launch_match launch_match_runs
+#endif
+#if FCX_RUNS
 #define FCX_RMODE_CALL __forceinline__
 #else
 #define FCX_RMODE_CALL __noinline__
