@@ -78,6 +78,11 @@
 #ifndef FCX_SPARSE
 #define FCX_SPARSE 0
 #endif
+// FCX_NOBUCKET: no bucket search; a tile the repeat filter does not send to the sparse search takes
+// the whole-tile run-table mode (the sparse unit)
+#ifndef FCX_NOBUCKET
+#define FCX_NOBUCKET FCX_SPARSE
+#endif
 #if FCX_SPARSE   // (the sparse search inline in its own unit: rand k_match 2.43 -> 2.31 ms per GiB)
 #define FCX_SPARSE_CALL __forceinline__
 #else
@@ -807,7 +812,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
     // search, [step (u16 x 4096) | parse scratch] after it
     __shared__ __attribute__((aligned(16))) uint32_t region[kRegionWords];
-#if !FCX_SPARSE
+#if !FCX_NOBUCKET
     uint32_t *hw = region;                                  // packed u16 bucket counters, then starts
     uint16_t *h16 = (uint16_t *)region;
     uint16_t *ent = (uint16_t *)(region + kHeadWords);     // window entries, bucket-sorted
@@ -940,7 +945,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     const uint32_t nruns_img = s_nruns + s_nruns2;   // s_nruns2 = 0 unless pass 2 ran (then after its barrier)
 #endif
-#if FCX_SPARSE
+#if FCX_NOBUCKET
     bool rmode = (nruns_img <= kRunTile && !(dbg & 4u)) || (dbg & 8u);   // (set below for non-sparse tiles)
 #else
     const bool rmode = (nruns_img <= kRunTile && !(dbg & 4u)) || (dbg & 8u);
@@ -1018,7 +1023,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                       mbits + (uint64_t)b * L.wpb + (t0 >> 6), q0, npos, ins_end, w0, blen, t1 - t0, dbg);
         __syncthreads();
         if (dbg & 32u) return;
-#if FCX_SPARSE
+#if FCX_NOBUCKET
     } else {   // not sparse: the whole-tile run-table mode, as for run-mode tiles
         rmode = true;
         for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
