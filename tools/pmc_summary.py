@@ -54,7 +54,7 @@ if out_json:
     json.dump(res, open(out_json, "w"), indent=1)
 for kind, ks in sorted(res.items()):
     for name, c in sorted(ks.items()):
-        if name not in ("k_match", "k_emit", "k_stitch", "k_encode"):
+        if not name.startswith("k_match") and name not in ("k_emit", "k_stitch", "k_encode"):
             continue
         print(f"[{kind}] {name}")
         for k, v in sorted(c.items()):
