@@ -1,7 +1,7 @@
 """The committed round evidence is self-consistent (CPU only): every bench leg in
-profiles/r04_bench_n1.json carries a roofline and a cpu_baseline, and each leg's roofline
+profiles/r05_bench_n1.json carries a roofline and a cpu_baseline, and each leg's roofline
 fraction is reproducible from the rocprofv3 kernel stats committed beside it
-(profiles/r04_kernel_stats_<leg>.csv, the same recomputation as tools/roofline_check.py)."""
+(profiles/r05_kernel_stats_<leg>.csv, the same recomputation as tools/roofline_check.py)."""
 import csv
 import json
 import os
@@ -10,7 +10,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-TAG = "r04"
+TAG = "r05"
 LEGS = ("rand", "c2", "text", "c3", "zeros", "runs", "dna")
 
 
