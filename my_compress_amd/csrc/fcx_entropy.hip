@@ -128,10 +128,12 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
                                                  uint32_t dbg_in) {
     const uint32_t dbg = kDev ? dbg_in : 0u;
     __shared__ __attribute__((aligned(16))) uint32_t w[256];
-    __shared__ uint32_t sw[257], ss[257], ln[256];   // (the merge reads the leaf queue two deep)
-    __shared__ uint32_t iw[256], il[256], ir[256], par[512];
-    __shared__ __attribute__((aligned(16))) uint32_t sk[256];
-    __shared__ uint32_t part[kTreeW][256];
+    // one region, two lives: the stream byte counts (u16 x 16 lane slots per byte value) while the
+    // flag / distance / golomb bytes are counted, then the leaf queue, merge and code arrays
+    __shared__ __attribute__((aligned(16))) uint32_t big[256 * 16];
+    uint32_t *sw = big, *ss = big + 260, *ln = big + 520, *iw = big + 776, *il = big + 1032, *ir = big + 1288;
+    uint32_t *par = big + 1544, *sk = big + 2056;   // (sk 16-B aligned: 2056 = 4 x 514)
+    uint32_t (*part)[256] = (uint32_t (*)[256])(big + 2312);   // chars rows (the chars stream only)
     __shared__ uint32_t s_red[kTreeW];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / kStreams, s = blockIdx.x % kStreams;
@@ -173,9 +175,13 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
         // codes) are counted in registers, the rest by LDS atomics
         const uint8_t *sb = (s == 0 ? s0 : s == 2 ? s2 : s3) + (uint64_t)b * L.sstride[s];
         const uint32_t nby = bi.slen[s], nq = nby / 16;
-        w[tid] = 0;
+        // byte value by counts into word 16 by + (lane & 15), half (lane >> 4) & 1: the 32 lanes of a
+        // bank group add to 32 different banks (random bytes no longer pile onto a few banks); 8 lanes
+        // share a u16 counter, at most slen / 32 < 2^16 bytes (slen < 2 MiB)
+        for (uint32_t x = tid; x < 256 * 16 / 4; x += kTreeT) ((uint4 *)big)[x] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         uint32_t c00 = 0, cff = 0;
+        const uint32_t slot = lane & 15u, inc = 1u << (16 * ((lane >> 4) & 1u));
         auto count4 = [&](uint32_t v, uint32_t nb) {
 #pragma unroll
             for (uint32_t q = 0; q < 4; q++) {
@@ -183,7 +189,7 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
                 if (q >= nb) break;
                 if (by == 0) c00++;
                 else if (by == 0xFFu) cff++;
-                else atomicAdd(&w[by], 1u);
+                else atomicAdd(&big[16 * by + slot], inc);
             }
         };
         const uint4 *s4 = (const uint4 *)sb;   // (stream strides are multiples of 16)
@@ -204,6 +210,19 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
         if (tid < nby - 16 * nq) count4(sb[16 * nq + tid], 1);
         c00 = wave_sum_u32(c00);
         cff = wave_sum_u32(cff);
+        __syncthreads();
+        {   // byte tid's count: its 16 words, both halves
+            const uint4 *r4 = (const uint4 *)(big + 16 * tid);
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint4 v4 = r4[q];
+                t += (v4.x & 0xFFFFu) + (v4.x >> 16) + (v4.y & 0xFFFFu) + (v4.y >> 16) + (v4.z & 0xFFFFu) + (v4.z >> 16) +
+                     (v4.w & 0xFFFFu) + (v4.w >> 16);
+            }
+            w[tid] = t;
+        }
+        __syncthreads();
         if (lane == 0) { atomicAdd(&w[0], c00); atomicAdd(&w[0xFF], cff); }
         __syncthreads();
     }
