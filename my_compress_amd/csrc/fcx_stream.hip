@@ -179,21 +179,31 @@ int fcx_compress_stream(fcx_ctx *ctx, fcx_read_fn rd, fcx_write_fn wr, void *use
     Pipeline &P = *PP;
     const uint64_t *dlen = fcx_ctx_device_out_len(ctx);
     uint64_t tin = 0, tout = 0, tblocks = 0;
-    // finish shard in slot x: length back, records D2H, write
-    auto drain = [&](Slot &x) -> int {
+    // finish shard in slot x in two halves: length back and the records' D2H issued (start), then,
+    // after the host has read the next shard into the slot's input buffer meanwhile, the D2H
+    // waited for and the records written (finish)
+    uint64_t olen_pending = 0;
+    auto drain_start = [&](Slot &x) -> int {
         SHIP(hipEventSynchronize(x.comp));
         const uint32_t e = (uint32_t)x.hlen[1];
         if (e & 4u) return sfail(FCX_ERR_CAPACITY, "shard output capacity");
         if (e) return sfail(FCX_ERR_INTERNAL, "device invariant violated (error bits " + std::to_string(e) + ")");
-        const uint64_t olen = x.hlen[0];
-        SHIP(hipMemcpyAsync(x.hout, x.dout, olen, hipMemcpyDeviceToHost, P.sout));
+        olen_pending = x.hlen[0];
+        SHIP(hipMemcpyAsync(x.hout, x.dout, olen_pending, hipMemcpyDeviceToHost, P.sout));
         SHIP(hipEventRecord(x.d2h, P.sout));
+        return FCX_OK;
+    };
+    auto drain_finish = [&](Slot &x) -> int {
         SHIP(hipEventSynchronize(x.d2h));
-        const int w = wr(user, x.hout, olen);
+        const int w = wr(user, x.hout, olen_pending);
         if (w) return sfail(w < 0 ? w : FCX_ERR_ARG, "write callback failed");
-        tout += olen;
+        tout += olen_pending;
         x.n = 0;
         return FCX_OK;
+    };
+    auto drain = [&](Slot &x) -> int {
+        const int rr = drain_start(x);
+        return rr ? rr : drain_finish(x);
     };
     int64_t got = read_full(rd, user, P.s[0].hin, shard);
     if (got < 0) return sfail(FCX_ERR_ARG, "read callback failed");
@@ -214,12 +224,14 @@ int fcx_compress_stream(fcx_ctx *ctx, fcx_read_fn rd, fcx_write_fn wr, void *use
         // and write y's finished records
         const bool last = x.n < shard;
         got = 0;
-        if (y.n) { if ((r = drain(y))) return r; }
-        if (!last) {
+        const bool ydrain = y.n != 0;
+        if (ydrain) { if ((r = drain_start(y))) return r; }
+        if (!last) {   // (y.hin: its H2D is long done; y's records go out through y.hout meanwhile)
             SHIP(hipEventSynchronize(y.h2d));
             got = read_full(rd, user, y.hin, shard);
             if (got < 0) return sfail(FCX_ERR_ARG, "read callback failed");
         }
+        if (ydrain) { if ((r = drain_finish(y))) return r; }
     }
     for (auto &x : P.s)
         if (x.n) { if ((r = drain(x))) return r; }
