@@ -121,7 +121,7 @@ constexpr uint32_t kMT = kMatchThreads;              // 512
 constexpr uint32_t kSeg = kTile / kMT;               // 8 positions per lane in the parse
 constexpr uint32_t kQPL = kTile / kMT;               // 8 queries per lane
 #if defined(FCX_UNIT_ILP)
-constexpr uint32_t kIlp = FCX_UNIT_ILP;   // a unit's own width (fcx_match_nf.hip)
+constexpr uint32_t kIlp = FCX_UNIT_ILP;   // a unit's own width (fcx_match_nf.hip, fcx_match_k4.hip)
 #else
 constexpr uint32_t kIlp = 4;                         // interleaved chain walks per lane
 #endif

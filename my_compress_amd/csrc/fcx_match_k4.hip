@@ -5,4 +5,5 @@
 // source and code stay as they are.
 #define FCX_KEY4 1
 #define FCX_NOFILTER 1
+#define FCX_UNIT_ILP 2   // two interleaved bucket walks per lane: dna k_match 24.6 -> 24.0 ms per GiB
 #include "fcx_match.hip"
