@@ -88,7 +88,7 @@
 #else
 #define FCX_SPARSE_CALL __noinline__
 #endif
-#if !FCX_NOFILTER && !FCX_SPARSE
+#if !FCX_NOFILTER && !FCX_SPARSE && !FCX_RUNS
 #define FCX_SAMPLE 1   // the repeat sample decides whether the filter runs
 #else
 #define FCX_SAMPLE 0
@@ -877,6 +877,8 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     if (tid == 0) {
 #if FCX_SPARSE || FCX_NOFILTER
         s_unknown = 0; s_match = 0; s_chg[0] = 0; s_chg[1] = 0;
+#elif !FCX_SAMPLE
+        s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_chg[0] = 0; s_chg[1] = 0;
 #else
         s_unknown = 0; s_match = 0; s_nruns = 0; s_nruns2 = 0; s_sample = 0; s_chg[0] = 0; s_chg[1] = 0;
 #endif
