@@ -734,6 +734,27 @@ __device__ inline void uniform_tile_out(uint32_t *sc /* >= kMT + 1 words */, uin
                                         uint32_t blen) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     auto ustep = [&](uint32_t p) -> uint32_t { return m_len(m_uniform(p, blen)) + 1; };
+#if FCX_RUNS
+    // (the runs unit's shards are mostly uniform tiles, zeros: the closed forms)  m_uniform is a match
+    // except at the block's first position and where fewer than 4 bytes remain: lane w writes mbits
+    // word w directly; a step is min(258, blen - p), so a lane's walk to its segment jumps the
+    // full-length steps at once
+    if (tid < (t1 - t0 + 63) / 64) {
+        const uint32_t a = t0 + 64 * tid, lo = blen >= 3 ? blen - 3 : 0u;   // literal from lo on
+        uint64_t word = t1 - a < 64 ? (1ull << (t1 - a)) - 1 : ~0ull;
+        if (a == 0) word &= ~1ull;
+        if (lo < a + 64) word &= lo <= a ? 0ull : (1ull << (lo - a)) - 1;
+        mbw[a >> 6] = word;
+    }
+    const uint32_t s = t0 + tid * kSeg, se = min(s + kSeg, t1);
+    uint32_t T = 0, p = t0;
+    if (p == 0 && s > 0) p = 1;   // position 0: a literal
+    if (p < s && blen - p >= kMaxL) {
+        const uint32_t kmax = (blen - p - kMaxL) / kMaxL + 1, ks = (s - p + kMaxL - 1) / kMaxL;
+        p += kMaxL * min(kmax, ks);
+    }
+    while (p < s) p += ustep(p);
+#else
 #pragma unroll
     for (uint32_t r = 0; r < kQPL; r++) {   // a wave's 64 lanes: 64 consecutive positions
         const uint32_t i = t0 + tid + kMT * r;
@@ -743,6 +764,7 @@ __device__ inline void uniform_tile_out(uint32_t *sc /* >= kMT + 1 words */, uin
     const uint32_t s = t0 + tid * kSeg, se = min(s + kSeg, t1);
     uint32_t T = 0, p = t0;
     while (p < s) p += ustep(p);
+#endif
     uint32_t cnt[3] = {0, 0, 0};
     while (p < se) {
         T |= 1u << (p - s);
