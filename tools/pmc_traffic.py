@@ -31,7 +31,14 @@ for kind in names:
         out[f"{kind}:{name[2:]}"] = {"fetch_size_bytes": fetch, "write_size_bytes": write,
                                       "hbm_bytes_per_launch": 2 * fetch + write,
                                       "launches": len(d["FETCH_SIZE"])}
-json.dump(out, open(os.path.join(ROOT, f"profiles/pmc_{tag}.json"), "w"), indent=1)
+# legs measured in this pass replace theirs; the other legs of an existing summary stay (a pass over a
+# subset of the legs must not drop the rest from pmc_latest.json, which bench.py reads)
+path = os.path.join(ROOT, f"profiles/pmc_{tag}.json")
+merged = json.load(open(path)) if os.path.exists(path) else {}
+merged = {k: v for k, v in merged.items() if k.split(":")[0] not in names}
+merged.update(out)
+out = merged
+json.dump(out, open(path, "w"), indent=1)
 json.dump(out, open(os.path.join(ROOT, "profiles/pmc_latest.json"), "w"), indent=1)
 for k, v in sorted(out.items()):
     print(f"{k:22s} fetch {v['fetch_size_bytes']/1e9:8.3f} GB  write {v['write_size_bytes']/1e9:8.3f} GB  "
