@@ -51,13 +51,18 @@ HL_DIGEST = {  # reference output digests of whole files (SURVEY.md §8(c) / B.4
     ("zeros", 0, GiB, 1 << 20): ("533fd45fbaa861a6060e9a5beac177cc0b64db691fc602a1e0e1e188afa5f912", 7521290),
     ("runs", 5, GiB, 1 << 20): ("4fced94fd4725ba3b1031dec67d63e1295b95ae08cc1cf0e34c84769f5313d26", 42548682),
     ("rand", 2, 64 << 20, 1 << 16): ("3b6853f2cf570b7a35c469efff62c15e0290b04ede45f6b47a97afc82c1878a5", 68819158),
+    # the mix leg: the reference compiled in place, tests/golden/make_mix_digest.py
+    ("mix", 0, GiB, 1 << 20): ("ce8bb8bc756a62fcd276d6a71b93456c18a7def3d77e555ea7eb8b92bfebffb5", 523200760),
 }
-SEEDS = {"rand": 4, "text": 3, "runs": 5, "zeros": 0, "dna": 6}
+SEEDS = {"rand": 4, "text": 3, "runs": 5, "zeros": 0, "dna": 6, "mix": 0}
 # extra legs after the main one: name -> (kind, block bytes[, seed, MiB]); BASELINE configs 2
 # (64 MiB of seed-2 random bytes at 64 KiB blocks), 3 and 5, plus "dna" (rand()%4 bytes: dense
-# 3-byte buckets, the lazy-evaluation path)
+# 3-byte buckets) and "mix" (1 MiB blocks cycling rand / text / runs / dna: every match unit in
+# one call, tests/inputs.py mix_into)
 LEGS = {"c2": ("rand", 1 << 16, 2, 64), "text": ("text", 1 << 20), "c3": ("text", 1 << 18),
-        "zeros": ("zeros", 1 << 20), "runs": ("runs", 1 << 20), "dna": ("dna", 1 << 20)}
+        "zeros": ("zeros", 1 << 20), "runs": ("runs", 1 << 20), "dna": ("dna", 1 << 20), "mix": ("mix", 1 << 20)}
+# legs whose first call on a fresh context is timed beside the steady state (cold_call)
+COLD_LEGS = ("rand", "text", "mix")
 
 
 def log(*a):
@@ -78,6 +83,11 @@ def make_input(kind, seed, lo, hi, pinned=True):
         host = host.pin_memory()
     if kind in ("rand", "dna"):
         inputs.rand_stream_into(seed, lo, host.data_ptr(), n, kind)
+    elif kind == "mix" and lo:
+        whole = torch.empty(hi, dtype=torch.uint8)
+        inputs.mix_into(whole.data_ptr(), hi)
+        host[:n].copy_(whole[lo:hi])
+        del whole
     elif kind == "zeros" or lo == 0:
         inputs.generate_into(kind, seed, host.data_ptr(), n)
     else:
@@ -345,6 +355,10 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
                 res["partition"]["source"] = ("--share0" if args.share0_ppm >= 0 else
                                               f"step model at the assumed {args.link_gbps} GB/s link")
     res["match_kernel"] = ctx.match_kernel() if n else None   # (the timed steps' match stage)
+    if n:   # tiles per match unit in the last call (fcx_route.hip)
+        res["route"] = ctx.route_stats()
+    if n and kind in COLD_LEGS and (main_leg or world == 1):
+        res["cold_call"] = cold_call(d_in, n, d_out, cap, block, dev, res["compress_only"]["ms_per_step"])
     stats = ctx.stats() if n else {"tokens": 0, "matches": 0, "lazy_evals": 0, "lazy_tiles": 0}
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
@@ -414,6 +428,63 @@ def verify(kind, seed, block, n_global, scaling, rank, world, dev, dist, d_out, 
     out["bit_exact_vs_reference"] = h.hexdigest() == want_sha and total + 10 == want_bytes
     out["checked"] = "sha256 of header + assembled stream on rank 0 vs the reference's file (SURVEY.md B.4)"
     return out
+
+
+def cold_call(d_in, n, d_out, cap, block, dev, steady_ms):
+    """the first compress call of a fresh context (it waits for its own route counts: no estimate
+    yet) and its second call, each synchronous, against the steady state of back-to-back calls"""
+    import torch
+
+    import my_compress_amd as mc
+
+    ctx = mc.Context(dev.index, block, n)
+    sid = torch.cuda.current_stream(dev).cuda_stream
+    ms = []
+    try:
+        for _ in range(2):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, sid)
+            ms.append((time.perf_counter() - t0) * 1e3)
+        rs = ctx.route_stats()
+    finally:
+        ctx.close()
+    return {"cold_ms": ms[0], "second_ms": ms[1], "steady_ms": steady_ms, "cold_vs_steady": ms[0] / steady_ms,
+            "cold_value": n / ms[0] / 1e3, "rest_tiles_second_call": rs["rest"],
+            "note": "one synchronous call of a fresh context (its first: the route counts are read back "
+                    "before the units launch), then a second; steady = compress_only ms per step"}
+
+
+def transition_leg(dev, block=1 << 20, shard_mib=256, calls=4):
+    """one context, device-resident shards: `calls` rand shards, then `calls` text shards, each call
+    synchronous.  The first text call runs with the estimate of the rand calls (its text tiles go to
+    k_match_rest), so its time against the steady text call is the price of a change of kind; the
+    stream path (fcx_compress_stream) sees the same on every shard whose kind changed"""
+    import torch
+
+    import my_compress_amd as mc
+
+    n = shard_mib << 20
+    ins = {k: make_input(k, SEEDS[k], 0, n).to(dev) for k in ("rand", "text")}
+    cap = mc.shard_bound(n, block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx = mc.Context(dev.index, block, n)
+    sid = torch.cuda.current_stream(dev).cuda_stream
+    ms, rest = {"rand": [], "text": []}, []
+    try:
+        for k in ("rand", "text"):
+            for _ in range(calls):
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                ctx.compress_shard(ins[k].data_ptr(), n, d_out.data_ptr(), cap, sid)
+                ms[k].append((time.perf_counter() - t0) * 1e3)
+                rest.append(ctx.route_stats()["rest"])
+    finally:
+        ctx.close()
+    steady = min(ms["text"][1:])
+    return {"shard_mib": shard_mib, "rand_ms": ms["rand"], "text_ms": ms["text"], "rest_tiles": rest,
+            "first_text_vs_steady": ms["text"][0] / steady,
+            "note": "synchronous calls on one context: rand x %d then text x %d" % (calls, calls)}
 
 
 def host_leg(host, n, block, reps=3):
@@ -675,14 +746,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--kind", default="rand", choices=["rand", "text", "runs", "zeros", "dna"])
+    ap.add_argument("--kind", default="rand", choices=["rand", "text", "runs", "zeros", "dna", "mix"])
     ap.add_argument("--global-mib", type=int, default=1024, help="headline input size, split over the ranks")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="main leg: strong = --global-mib split N ways (default), weak = --mib per rank")
     ap.add_argument("--mib", type=int, default=1024, help="MiB per rank for weak scaling (the weak leg)")
     ap.add_argument("--block", type=int, default=1 << 20)
     ap.add_argument("--no-text", action="store_true", help="skip every extra leg")
-    ap.add_argument("--legs", default="c2,text,c3,zeros,runs,dna",
+    ap.add_argument("--legs", default="c2,text,c3,zeros,runs,dna,mix",
                     help="extra legs after the main one (comma list of " + ",".join(LEGS) + ")")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling (config 4) leg at N > 1")
     ap.add_argument("--concat", default="pipe", choices=["pipe", "gather", "allgather", "none"],
@@ -706,6 +777,7 @@ def main():
                     help="skip the host-to-host (PCIe-inclusive) timing of the main leg")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-lz78", action="store_true", help="skip the -c lz78 codec leg")
+    ap.add_argument("--no-transition", action="store_true", help="skip the rand -> text change-of-kind timing")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     args = ap.parse_args()
 
@@ -780,7 +852,8 @@ def main():
                     "(= the first GiB of BASELINE config 4); extra legs: text = enwik-style generator seed 3 at "
                     "1 MiB (HL-text) and 256 KiB blocks (C3), c2 = rand seed 2, 64 MiB at 64 KiB blocks (config 2), zeros "
                     "and runs seed 5 (config 5), dna = "
-                    "'ACGT'[rand()%4] seed 6 (lazy-path stress)",
+                    "'ACGT'[rand()%4] seed 6, mix = 1 MiB blocks cycling rand / text / runs / dna (every match "
+                    "unit in one call)",
             "config": {"workload": f"{args.kind} {main_res['global_bytes'] >> 20} MiB, {args.block // 1024} KiB "
                                    f"blocks, {shard_note}; step = compress + concatenation of the segments "
                                    f"into one stream ({main_res['concat']})",
@@ -800,12 +873,16 @@ def main():
             "lazy_evals": main_res["lazy_evals"],
             "decode": main_res.get("decode"),
             "host_path": main_res.get("host_path"),
+            "route": main_res.get("route"),
+            "cold_call": main_res.get("cold_call"),
         }
         if world == 1 and not args.no_lz78 and not args.no_text:
             line["lz78"] = lz78_leg(dev)
+        if world == 1 and not args.no_transition and not args.no_text:
+            line["transition"] = transition_leg(dev)
         keep = ["value", "ms_per_step", "compress_only", "concat_ms_per_step", "ratio", "block_bytes", "stages_ms",
                 "lazy_evals", "lazy_tiles", "decode", "bit_exact_vs_reference", "global_bytes", "partition",
-                "concat_impl"]
+                "concat_impl", "route", "cold_call"]
         for name, lr in legs.items():
             line[name] = {k: lr[k] for k in keep if k in lr}
             line[name]["roofline"] = roofline(lr, name, pmc)
@@ -828,12 +905,16 @@ def main():
                           "frac": round(rf["frac"], 4) if rf.get("frac") else None,
                           "path_frac": round(rf["path_frac"], 4) if rf.get("path_frac") else None,
                           "cpu_MBps": round(cb["value"], 1) if cb.get("value") else None}
+            if v.get("cold_call"):
+                summ[name]["cold_vs_steady"] = round(v["cold_call"]["cold_vs_steady"], 3)
 
         brief(args.kind, line)
         for name in legs:
             brief(name, line[name])
         if "weak" in line:
             brief("weak", line["weak"])
+        if "transition" in line:
+            summ["transition"] = {"first_text_vs_steady": round(line["transition"]["first_text_vs_steady"], 3)}
         line["legs"] = summ
         print(json.dumps(line), flush=True)
     if dist:

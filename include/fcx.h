@@ -127,18 +127,13 @@ int fcx_compress_stream(fcx_ctx *ctx, fcx_read_fn read, fcx_write_fn write, void
 
 /* Enables per-kernel hipEvent timing of subsequent fcx_compress_shard calls. */
 int fcx_ctx_set_profiling(fcx_ctx *ctx, int enable);
-/* Testing: forces how the match kernel evaluates every tile of later calls —
- * 0 auto (default: run table for tiles of long runs, sparse search where few keys
- * repeat, else bucket search), 1 bucket search for every tile (unknown positions
- * via the run table / the stitch), 2 run table for whole tiles, 3 the general kernel for
- * every call, 4 the 4-byte-key kernel for every call, 5 the kernel without the repeat
- * filter for every call, 6 the kernel with the run-mode walk inlined for every call, 7
- * the kernel without the bucket search for every call (auto: the 4-byte-key kernel when
- * >= 90 % of the blocks of a recent call had small alphabets, e.g. 'ACGT' data, else the
- * no-filter kernel when >= 90 % were match-dense, e.g. text, else the runs kernel when
- * >= 90 % had long matches, e.g. runs or zeros, else the sparse kernel when >= 90 % had
- * few matches, e.g. random data, else the general one; the recent call is the one before
- * when its length was read back, else the last of every 16th call).  The output is identical in every mode; only the speed
+/* Testing: forces how the match search runs in later calls — 0 auto (default: every
+ * tile goes to the match unit its own sampled bytes call for, fcx_ctx_route_stats), 1 the
+ * general kernel with the bucket search for every tile (unknown positions via the run table /
+ * the stitch), 2 the general kernel with the run table for whole tiles, 3 the general kernel,
+ * 4 the 4-byte-key unit, 5 the unit without the repeat filter, 6 the unit with the run-mode
+ * walk inlined, 7 the unit without the bucket search — modes 1-7 unrouted, every tile of the
+ * call through that one kernel.  The output is identical in every mode; only the speed
  * differs. */
 int fcx_ctx_set_match_mode(fcx_ctx *ctx, int mode);
 /* Pipelined launch: fcx_compress_shard splits the shard's blocks into `groups` groups
@@ -154,11 +149,19 @@ int fcx_ctx_stage(fcx_ctx *ctx, int i, const char **name, float *ms);
  * tokens, matches, lazily evaluated positions, lazy tiles, total tiles */
 int fcx_ctx_stats(fcx_ctx *ctx, uint64_t *tokens, uint64_t *matches, uint64_t *lazy_evals,
                   uint64_t *lazy_tiles, uint64_t *tiles);
-/* The match kernel the last fcx_compress_shard call ran: 0 general, 1 4-byte keys (small
- * alphabets), 2 without the repeat filter (match-dense data), 3 run-mode walk inlined
- * (long matches), 4 without the bucket search (few matches); -1 for a NULL ctx
- * (fcx_ctx_set_match_mode). */
+/* The match kernel the last fcx_compress_shard call ran (routed: the unit given the most
+ * tiles): 0 general, 1 4-byte keys (small alphabets), 2 without the repeat filter
+ * (match-dense data), 3 run-mode walk inlined (long matches), 4 without the bucket search
+ * (few matches); -1 for a NULL ctx. */
 int fcx_ctx_match_kernel(fcx_ctx *ctx);
+/* Routing of the last (routed) call, after a device synchronize: out[0..3] tiles filed to the
+ * sparse, runs, 4-byte-key and no-filter units (the no-filter count includes the hand-ons), out[4]
+ * tiles the sparse / runs units handed on to the no-filter unit, out[5] tiles with bytes, out[6]
+ * tiles past the units' grids (searched by k_match_rest, the general kernel), out[7] 1 when the
+ * call waited for its own counts (a context's first call).  Writes min(n, FCX_ROUTE_STATS)
+ * values; FCX_ERR_ARG when the last call had a forced unit (fcx_ctx_set_match_mode). */
+#define FCX_ROUTE_STATS 8
+int fcx_ctx_route_stats(fcx_ctx *ctx, uint64_t *out, int n);
 
 /* ---- GPU decoder ------------------------------------------------------------ */
 

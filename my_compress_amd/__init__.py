@@ -75,6 +75,8 @@ def lib():
     L.fcx_ctx_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
     L.fcx_ctx_match_kernel.argtypes = [ctypes.c_void_p]
     L.fcx_ctx_match_kernel.restype = ctypes.c_int
+    if hasattr(L, "fcx_ctx_route_stats"):   # (absent from an older FCX_LIB build used for A/B timing)
+        L.fcx_ctx_route_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.fcx_compress_stream.argtypes = [ctypes.c_void_p, READ_FN, WRITE_FN, ctypes.c_void_p, ctypes.c_uint64,
                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]
@@ -254,8 +256,19 @@ class Context:
     MATCH_KERNELS = ("k_match", "k_match_k4", "k_match_nf", "k_match_runs", "k_match_sparse")
 
     def match_kernel(self) -> str:
-        """the kernel the last compress_shard call's match stage ran (fcx_ctx_match_kernel)"""
+        """the kernel the last compress_shard call's match stage ran (fcx_ctx_match_kernel; routed:
+        the unit given the most tiles)"""
         return self.MATCH_KERNELS[lib().fcx_ctx_match_kernel(self._h)]
+
+    ROUTE_STATS = ("sparse", "runs", "key4", "nofilter", "handed_on", "tiles", "rest", "cold")
+
+    def route_stats(self) -> dict:
+        """how the last (routed) call's tiles were searched (fcx_ctx_route_stats): tiles per unit
+        list, tiles the sparse / runs units handed on, tiles with bytes, tiles left to k_match_rest,
+        and whether the call waited for its own counts (a context's first call)"""
+        vals = (ctypes.c_uint64 * 8)()
+        _check(lib().fcx_ctx_route_stats(self._h, vals, 8), "fcx_ctx_route_stats")
+        return dict(zip(self.ROUTE_STATS, [int(v) for v in vals]))
 
 
 class DContext:

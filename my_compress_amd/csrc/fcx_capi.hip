@@ -14,16 +14,22 @@
 #include "fcx_device.h"
 
 namespace fcx {
-void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                  uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
-void launch_match_k4(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                     uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
-void launch_match_nf(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                     uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
-void launch_match_runs(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                       uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
-void launch_match_sparse(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                         uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u);
+// one launcher per match unit (fcx_match*.hip); route null: the unit over every tile of the shard
+#define FCX_MATCH_LAUNCHER(name)                                                                               \
+    void name(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,              \
+              uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override = ~0u, \
+              const MatchRoute *route = nullptr, uint32_t grid = 0);
+FCX_MATCH_LAUNCHER(launch_match)
+FCX_MATCH_LAUNCHER(launch_match_k4)
+FCX_MATCH_LAUNCHER(launch_match_nf)
+FCX_MATCH_LAUNCHER(launch_match_runs)
+FCX_MATCH_LAUNCHER(launch_match_sparse)
+#undef FCX_MATCH_LAUNCHER
+void launch_match_rest(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                       uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, const RouteRest &rest, uint32_t grid,
+                       hipStream_t st);
+void launch_classify(const uint8_t *in, const Layout &L, uint32_t *lists, uint32_t stride, uint32_t *cnt,
+                     uint8_t *tkind, hipStream_t st);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -60,7 +66,7 @@ inline uint32_t round16(uint64_t x) { return (uint32_t)((x + 15) & ~15ull); }
 
 constexpr uint32_t kMaxGroups = 8;   // block groups of a pipelined fcx_compress_shard
 
-const char *kStageNames[] = {"memset",       "match",       "stitch", "emit",   "hist",   "tree",
+const char *kStageNames[] = {"route",        "match",       "stitch", "emit",   "hist",   "tree",
                              "block_layout", "scan_blocks", "zero",   "encode", "headers"};
 constexpr int kNumStages = 11;
 
@@ -90,14 +96,20 @@ namespace fcx {
 void set_last_error(const std::string &m) { g_err = m; }
 }  // namespace fcx
 
-constexpr uint64_t kKeyProbe = 16;   // calls without a length read per read of the block-kind counts
-
 // the match kernel's translation units (fcx_match.hip and the fcx_match_<kind>.hip units that include it)
 enum MatchKernel : int {
     kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2, kMatchRuns = 3, kMatchSparse = 4
 };
 using MatchLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64_t *, uint64_t *, uint64_t *,
-                             uint32_t *, uint32_t *, hipStream_t, uint32_t);
+                             uint32_t *, uint32_t *, hipStream_t, uint32_t, const MatchRoute *, uint32_t);
+// routed calls (fcx_route.hip): the unit of each list, in launch order (the sparse and runs units hand
+// tiles on to the no-filter unit's list, so it comes last)
+constexpr int kRouteKernel[kRoutes] = {kMatchSparse, kMatchRuns, kMatchKey4, kMatchNoFilter};
+constexpr uint32_t kRouteWords = 8;         // device counters per block group (k_classify: cnt[0..5])
+constexpr uint32_t kRouteMinTiles = 8;      // a unit expected to get fewer tiles is not launched (k_match_rest)
+constexpr uint32_t kRestGrid = 1024;        // k_match_rest's workgroups (4 per CU)
+constexpr uint64_t kRouteBytes = 4ull * kRouteWords * 8;   // route counters of kMaxGroups (= 8) groups
+constexpr uint64_t kWordBytes = 64 + kRouteBytes;          // dev_words
 static MatchLaunch match_launcher(int k) {
     return k == kMatchKey4 ? launch_match_k4 : k == kMatchNoFilter ? launch_match_nf
                                              : k == kMatchRuns    ? launch_match_runs
@@ -128,13 +140,21 @@ struct fcx_ctx {
     uint32_t *ctab = nullptr;          // code table
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
-    uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits, [2] = small-alphabet
-                                       // blocks | blocks << 32, [3] = match-dense | long-match blocks << 32,
-                                       // [4] = few-match blocks (k_tree)
-    uint64_t *host_words = nullptr;    // pinned mirror ([2..4]: refreshed by the length reads, and by an
-                                       // asynchronous copy every kKeyProbe-th call without one)
-    uint64_t calls = 0;
-    int last_kernel = kMatchGeneral;   // the last call's match kernel
+    uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits; from byte 64: the route
+                                       // counters, kRouteWords u32 per block group (k_classify, the units)
+    uint64_t *host_words = nullptr;    // pinned: [0..1] length reads; from byte 64 the route counters of a
+                                       // recent call (copied back asynchronously after every routed call);
+                                       // from byte 64 + kRouteBytes the first call's counts (waited for)
+    uint32_t *rlist = nullptr;         // route lists: kRoutes x cap_tiles tile indices (k_classify)
+    uint8_t *tkind = nullptr;          // per tile: its unit (k_classify)
+    uint64_t cap_tiles = 0;
+    bool have_hint = false;            // a routed call has run: the estimates below are set
+    uint64_t hint_cnt[kRoutes] = {};   // tiles per list (after the hand-ons) of a recent call ...
+    uint64_t hint_valid = 0;           // ... out of its tiles with bytes
+    uint32_t last_grid[kMaxGroups][kRoutes] = {};   // the last call's unit grids per group
+    uint32_t last_groups = 0;
+    bool last_routed = false, last_cold = false;
+    int last_kernel = kMatchGeneral;   // the last call's match kernel (routed: the unit with the largest grid)
     // pipelined launch: the shard's blocks in groups, consecutive groups on two streams so
     // one group's serial / latency-bound kernels (stitch, tree, scan, emit, encode) overlap
     // the next group's match kernel; the record-offset scans stay in group order
@@ -158,7 +178,7 @@ namespace {
 void free_scratch(fcx_ctx *c) {
     void *ptrs[] = {c->m,    c->mbits, c->chain, c->chain_pfx, c->tinfo, c->tile_off, c->mtok, c->tconv, c->fp, c->binfo,
                     c->s[0], c->s[1],  c->s[2],      c->s[3],       c->thist,    c->cstat, c->sdesc,
-                    c->ctab, c->ltab,  c->hhdr,      c->blk_off};
+                    c->ctab, c->ltab,  c->hhdr,      c->blk_off, c->rlist, c->tkind};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     c->m = nullptr; c->mbits = c->chain = c->chain_pfx = c->fp = nullptr; c->tinfo = c->tile_off = nullptr;
@@ -168,6 +188,9 @@ void free_scratch(fcx_ctx *c) {
     c->thist = nullptr; c->cstat = nullptr; c->sdesc = nullptr; c->ctab = nullptr;
     c->ltab = c->hhdr = nullptr;
     c->blk_off = nullptr;
+    c->rlist = nullptr;
+    c->tkind = nullptr;
+    c->cap_tiles = 0;
     c->cap_n = 0;
     c->cap_blocks = 0;
 }
@@ -204,6 +227,9 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     if ((r = dalloc(&c->ltab, 256ull * kStreams * nb, "ltab"))) return r;
     if ((r = dalloc(&c->hhdr, (uint64_t)kHuffHdrStride * kStreams * nb, "hhdr"))) return r;
     if ((r = dalloc(&c->blk_off, 8 * nb, "blk_off"))) return r;
+    if ((r = dalloc(&c->rlist, 4ull * kRoutes * nt, "route lists"))) return r;
+    if ((r = dalloc(&c->tkind, nt, "tile kinds"))) return r;
+    c->cap_tiles = nt;
     c->cap_n = (uint64_t)L.nblocks * c->B;
     c->cap_blocks = L.nblocks;
     return FCX_OK;
@@ -254,10 +280,11 @@ int fcx_ctx_create(fcx_ctx **out, int device, uint32_t block_bytes, uint64_t max
     fcx_ctx *c = new fcx_ctx();
     c->device = device;
     c->B = block_bytes;
-    e = hipHostMalloc((void **)&c->host_words, 64, hipHostMallocDefault);
+    static_assert(kMaxGroups == 8, "kRouteBytes");
+    e = hipHostMalloc((void **)&c->host_words, kWordBytes + kRouteBytes, hipHostMallocDefault);
     if (e != hipSuccess) { delete c; return hip_fail(e, "hipHostMalloc"); }
-    memset(c->host_words, 0, 64);   // (no small-alphabet blocks seen yet)
-    e = hipMalloc((void **)&c->dev_words, 64);
+    memset(c->host_words, 0, kWordBytes + kRouteBytes);
+    e = hipMalloc((void **)&c->dev_words, kWordBytes);
     if (e != hipSuccess) { (void)hipHostFree(c->host_words); delete c; return hip_fail(e, "hipMalloc"); }
     for (uint32_t g = 0; g < kMaxGroups; g++)
         for (int i = 0; i <= kNumStages; i++) (void)hipEventCreate(&c->ev[g][i]);
@@ -292,7 +319,7 @@ int fcx_ctx_read_out_len(fcx_ctx *c, uint64_t *out_len) {
     if (!c || !out_len) return fail(FCX_ERR_ARG, "fcx_ctx_read_out_len: NULL");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 40, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c->host_words, c->dev_words, 16, hipMemcpyDeviceToHost));
     const uint32_t e = (uint32_t)c->host_words[1];
     if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
     if (e) return fail(FCX_ERR_INTERNAL, "device invariant violated (error bits " + std::to_string(e) + ")");
@@ -375,28 +402,29 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     c->timed = c->profiling;
     c->ngroups_timed = c->profiling ? G : 0;
 
-    // match kernel: when >= 90 % of a recent call's blocks had small alphabets (dense 3-byte keys:
-    // 'ACGT' data) the 4-byte-key one, else when >= 90 % were match-dense (text) the one without the
-    // repeat filter, else when >= 90 % were long-match blocks (runs, zeros) the one with the run-mode
-    // walk inlined, else when >= 90 % were few-match blocks (random data) the one without the bucket
-    // search, else the general one; all give the same bytes.  (host_words[2..4] may be
-    // landing from an earlier call's copy: any value is a valid choice)
-    int kern = c->kernel;
-    if (kern == kMatchAuto) {
-        const uint64_t hw2 = __atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);
-        const uint64_t hw3 = __atomic_load_n(&c->host_words[3], __ATOMIC_RELAXED);
-        const uint64_t nfew = __atomic_load_n(&c->host_words[4], __ATOMIC_RELAXED) & 0xFFFFFFFFu;
-        const uint64_t nsmall = hw2 & 0xFFFFFFFFu, nblk = hw2 >> 32, ndense = hw3 & 0xFFFFFFFFu, nlong = hw3 >> 32;
-        kern = !nblk                       ? kMatchGeneral
-               : 10 * nsmall >= 9 * nblk ? kMatchKey4
-               : 10 * ndense >= 9 * nblk ? kMatchNoFilter
-               : 10 * nlong >= 9 * nblk  ? kMatchRuns
-               : 10 * nfew >= 9 * nblk   ? kMatchSparse
-                                         : kMatchGeneral;
+    // match search: unrouted when a unit is forced (fcx_ctx_set_match_mode), else routed per tile
+    // (fcx_route.hip): the estimates of each unit's share come from the route counters of a recent
+    // call (landing asynchronously: any values are a valid estimate, they only size the grids)
+    const bool routed = c->kernel == kMatchAuto;
+    if (routed && c->have_hint) {
+        const uint32_t *hr = (const uint32_t *)((const uint8_t *)c->host_words + 64);
+        uint64_t cnt[kRoutes] = {}, valid = 0;
+        for (uint32_t g = 0; g < kMaxGroups; g++) {
+            for (uint32_t u = 0; u < kRoutes; u++) cnt[u] += __atomic_load_n(&hr[kRouteWords * g + u], __ATOMIC_RELAXED);
+            valid += __atomic_load_n(&hr[kRouteWords * g + 5], __ATOMIC_RELAXED);
+        }
+        if (valid) {
+            for (uint32_t u = 0; u < kRoutes; u++) c->hint_cnt[u] = cnt[u];
+            c->hint_valid = valid;
+        }
     }
-    const MatchLaunch match = match_launcher(kern);
-    c->last_kernel = kern;
-    HIP_TRY(hipMemsetAsync(c->dev_words, 0, 40, st));
+    c->last_routed = routed;
+    c->last_cold = routed && !c->have_hint;
+    c->last_groups = G;
+    c->last_kernel = routed ? kMatchGeneral : c->kernel;
+    const MatchLaunch match = match_launcher(c->kernel);
+    uint64_t cold_cnt[kRoutes] = {}, cold_valid = 0;
+    HIP_TRY(hipMemsetAsync(c->dev_words, 0, kWordBytes, st));
     if (G > 1) {
         HIP_TRY(hipEventRecord(c->gsync[0], st));
         for (auto s2 : c->gst) HIP_TRY(hipStreamWaitEvent(s2, c->gsync[0], 0));
@@ -410,14 +438,64 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         const uint64_t t0 = b0 * L.tpb;   // first tile of the group
         uint8_t *sg_s[kStreams];
         for (uint32_t q = 0; q < kStreams; q++) sg_s[q] = c->s[q] + b0 * L.sstride[q];
-        if (ev) {
-            HIP_TRY(hipEventRecord(ev[0], sg));
-            HIP_TRY(hipEventRecord(ev[1], sg));   // (the memset above is not timed per group)
-        }
+        if (ev) HIP_TRY(hipEventRecord(ev[0], sg));   // (the memset above is not timed per group)
         const uint8_t *gin = d_in + b0 * c->B;
-        match(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
-                     c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, sg,
-                     c->match_mode);
+        uint32_t *gm = c->m + b0 * c->B, *gtinfo = c->tinfo + 8 * t0, *gmtok = c->mtok + t0 * kTileMatches;
+        uint64_t *gmbits = c->mbits + b0 * L.wpb, *gchain = c->chain + b0 * L.wpb, *gpfx = c->chain_pfx + t0 * (kTile / 64);
+        if (!routed) {
+            if (ev) HIP_TRY(hipEventRecord(ev[1], sg));
+            match(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, sg, c->match_mode, nullptr, 0);
+        } else {
+            // classify the group's tiles into the unit lists, then each unit over its list with a grid
+            // from the estimate (the first call waits for its own counts), k_match_rest for the rest
+            uint32_t *rc = (uint32_t *)((uint8_t *)c->dev_words + 64) + kRouteWords * g;
+            uint32_t *lists = c->rlist + t0;
+            const uint32_t stride = (uint32_t)c->cap_tiles, ntg = Lg.nblocks * Lg.tpb;
+            launch_classify(gin, Lg, lists, stride, rc, c->tkind + t0, sg);
+            if (ev) HIP_TRY(hipEventRecord(ev[1], sg));
+            uint64_t est[kRoutes];
+            if (!c->have_hint) {
+                uint32_t *cold = (uint32_t *)((uint8_t *)c->host_words + kWordBytes);
+                HIP_TRY(hipMemcpyAsync(cold, rc, 4 * kRouteWords, hipMemcpyDeviceToHost, sg));
+                HIP_TRY(hipStreamSynchronize(sg));
+                for (uint32_t u = 0; u < kRoutes; u++) { est[u] = cold[u]; cold_cnt[u] += cold[u]; }
+                cold_valid += cold[5];
+            } else {
+                const uint64_t v = std::max<uint64_t>(c->hint_valid, 1);
+                for (uint32_t u = 0; u < kRoutes; u++) est[u] = (c->hint_cnt[u] * ntg + v - 1) / v;
+            }
+            RouteRest rest{lists, rc, stride, {0, 0, 0, 0}};
+            // the unit expected to take most of the tiles (at least half) runs over every tile of the
+            // group and skips the others by their kind byte: no list read before its staging loads
+            uint32_t best = 0;
+            for (uint32_t u = 1; u < kRoutes; u++)
+                if (est[u] > est[best]) best = u;
+            const bool direct = 2 * est[best] >= ntg;
+            for (uint32_t u = 0; u < kRoutes; u++) {
+                // a small margin over the estimate (its excess workgroups exit at once); the no-filter
+                // list also takes the tiles the sparse / runs units hand on
+                const uint64_t gr = est[u] >= kRouteMinTiles ? est[u] + est[u] / 16 + 32 : 0;
+                MatchRoute rt;
+                rt.kind = c->tkind + t0;
+                rt.mine = u;
+                if (direct && u == best) {
+                    rest.grid[u] = ~0u;   // (every entry of its list: the direct grid has them all)
+                } else {
+                    rest.grid[u] = (uint32_t)std::min<uint64_t>(gr, ntg);
+                    rt.list = lists + (uint64_t)u * stride;
+                    rt.cnt = rc + u;
+                }
+                if (u == kRouteSparse || u == kRouteRuns) {
+                    rt.defer_list = lists + (uint64_t)kRouteNoFilter * stride;
+                    rt.defer_cnt = rc + kRouteNoFilter;
+                }
+                match_launcher(kRouteKernel[u])(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, sg, 0u, &rt,
+                                                rest.grid[u]);
+                c->last_grid[g][u] = rest.grid[u];
+            }
+            if (g == 0) c->last_kernel = est[best] ? kRouteKernel[best] : kMatchGeneral;
+            launch_match_rest(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, rest, kRestGrid, sg);
+        }
         if (ev) HIP_TRY(hipEventRecord(ev[2], sg));
         launch_parse(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
                      c->chain_pfx + t0 * (kTile / 64), c->tinfo + 8 * t0, c->mtok + t0 * kTileMatches, c->fp + 12 * t0,
@@ -443,10 +521,17 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         }
     }
     HIP_TRY(hipGetLastError());
-    if (!out_len && c->kernel == kMatchAuto && c->calls++ % kKeyProbe == 0)
-        HIP_TRY(hipMemcpyAsync(c->host_words + 2, c->dev_words + 2, 24, hipMemcpyDeviceToHost, st));
+    if (routed && !c->have_hint && cold_valid) {
+        for (uint32_t u = 0; u < kRoutes; u++) c->hint_cnt[u] = cold_cnt[u];
+        c->hint_valid = cold_valid;
+    }
+    if (routed) {   // the route counters back for the next calls' estimates (asynchronous)
+        HIP_TRY(hipMemcpyAsync((uint8_t *)c->host_words + 64, (uint8_t *)c->dev_words + 64, kRouteBytes,
+                               hipMemcpyDeviceToHost, st));
+        c->have_hint = true;
+    }
     if (out_len) {
-        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 40, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->host_words, c->dev_words, 16, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         const uint32_t e = (uint32_t)c->host_words[1];
         if (e & 4u) return fail(FCX_ERR_CAPACITY, "output capacity too small (see fcx_shard_bound)");
@@ -495,6 +580,29 @@ int fcx_debug_emit_bits(fcx_ctx *c, uint32_t bits) {
 
 int fcx_ctx_match_kernel(fcx_ctx *c) { return c ? c->last_kernel : -1; }
 
+int fcx_ctx_route_stats(fcx_ctx *c, uint64_t *out, int n) {
+    if (!c || !out || n < 0) return fail(FCX_ERR_ARG, "fcx_ctx_route_stats: bad argument");
+    uint64_t v[FCX_ROUTE_STATS] = {};
+    if (c->last_routed) {
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipDeviceSynchronize());
+        uint32_t rc[kRouteWords * kMaxGroups];
+        HIP_TRY(hipMemcpy(rc, (uint8_t *)c->dev_words + 64, sizeof(rc), hipMemcpyDeviceToHost));
+        for (uint32_t g = 0; g < c->last_groups; g++) {
+            const uint32_t *r = rc + kRouteWords * g;
+            for (uint32_t u = 0; u < kRoutes; u++) {
+                v[u] += r[u];
+                v[6] += r[u] > c->last_grid[g][u] ? r[u] - c->last_grid[g][u] : 0u;
+            }
+            v[4] += r[kRouteNoFilter] - r[4];
+            v[5] += r[5];
+        }
+        v[7] = c->last_cold;
+    }
+    for (int i = 0; i < n && i < FCX_ROUTE_STATS; i++) out[i] = v[i];
+    return c->last_routed ? FCX_OK : fail(FCX_ERR_ARG, "the last call was not routed (a match unit is forced)");
+}
+
 // development only (not in fcx.h): the match kernel alone with experiment bits, for
 // per-phase timing (tools/matchphase.py); the context's scratch is left invalid
 int fcx_debug_match(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint32_t dbg, void *stream) {
@@ -504,7 +612,7 @@ int fcx_debug_match(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint32_t dbg, v
     if (r) return r;
     const Layout L = make_layout(n, c->B);
     match_launcher(c->kernel)(d_in, L, c->m, c->mbits, c->chain, c->chain_pfx, c->tinfo, c->mtok, (hipStream_t)stream,
-                              dbg);
+                              dbg, nullptr, 0);
     HIP_TRY(hipGetLastError());
     return FCX_OK;
 }

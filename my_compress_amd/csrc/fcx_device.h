@@ -84,6 +84,25 @@ struct Layout {
     uint32_t pad;
 };
 
+// ---- per-tile routing of the match search (fcx_route.hip) ------------------
+// k_classify sorts the shard's tiles into one list per match unit; each unit's kernel then runs over
+// its own list, so the unit that searches a tile depends only on that tile's bytes.
+enum : uint32_t { kRouteSparse = 0, kRouteRuns = 1, kRouteKey4 = 2, kRouteNoFilter = 3, kRoutes = 4 };
+struct MatchRoute {
+    const uint32_t *list = nullptr;   // the launch's tiles (null: the grid is every tile of the shard)
+    const uint32_t *cnt = nullptr;    // entries in list
+    uint32_t *defer_list = nullptr;   // sparse / runs units: where a tile they do not search goes (the
+    uint32_t *defer_cnt = nullptr;    //   no-filter unit's list); null: their whole-tile run-table mode
+    uint8_t *kind = nullptr;          // per tile: its unit (k_classify; a hand-on rewrites it).  With no
+    uint32_t mine = 0;                //   list, the grid covers every tile and searches those of kind mine
+};
+struct RouteRest {                    // k_match_rest: list entries past the grid each unit was given
+    const uint32_t *lists;            // kRoutes lists of list_stride entries
+    const uint32_t *cnt;              // kRoutes counts
+    uint32_t list_stride;
+    uint32_t grid[kRoutes];           // grid of unit u's launch (0: not launched)
+};
+
 // ---- wave64 helpers --------------------------------------------------------
 __device__ inline uint32_t lane_id() { return __lane_id(); }
 // a value every lane of the wave holds alike, moved to a scalar register: loops and branches on

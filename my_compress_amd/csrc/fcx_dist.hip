@@ -345,10 +345,13 @@ struct LoopTransport final : Transport {
         DHIP(hipSetDevice(hub->device));
         std::unique_lock<std::mutex> lk(hub->mu);
         if (hub->aborted) return dfail(FCX_ERR_RCCL, hub->abort_msg);
-        for (auto &o : ops) {
-            o->posted = hub->event();
-            if (!o->posted || hipEventRecord(o->posted, o->st) != hipSuccess)
+        for (size_t i = 0; i < ops.size(); i++) {
+            ops[i]->posted = hub->event();
+            if (!ops[i]->posted || hipEventRecord(ops[i]->posted, ops[i]->st) != hipSuccess) {
+                for (size_t j = 0; j <= i; j++)   // nothing was posted: every event taken goes back
+                    if (ops[j]->posted) hub->retire(ops[j]->posted);
                 return dfail(FCX_ERR_HIP, "loopback transport: event record");
+            }
         }
         for (auto &o : ops) hub->post(o.get());
         hub->cv.notify_all();
@@ -417,6 +420,8 @@ struct fcx_dist {
     std::vector<hipEvent_t> ev;      // per sub-batch: compressed and its length copied
     uint8_t *d_stage = nullptr;      // rank 0: the peers' pieces as they arrive
     uint64_t stage_cap = 0;
+    uint8_t *d_drain = nullptr;      // rank 0: a piece beyond its peer's bound, received and dropped
+    uint64_t drain_cap = 0;
     int fail_piece = -1;             // testing: a peer treats this piece as failed (fcx_dist_debug_fail)
 };
 
@@ -522,8 +527,10 @@ void release_gather(fcx_dist *d) {
     if (d->d_ctl) (void)hipFree(d->d_ctl);
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);
     if (d->d_stage) (void)hipFree(d->d_stage);
+    if (d->d_drain) (void)hipFree(d->d_drain);
     d->cst = nullptr; d->d_words = nullptr; d->h_words = nullptr; d->d_ctl = nullptr; d->h_ctl = nullptr;
     d->d_stage = nullptr; d->stage_cap = 0;
+    d->d_drain = nullptr; d->drain_cap = 0;
 }
 
 inline uint64_t round16(uint64_t x) { return (x + 15) & ~15ull; }
@@ -627,7 +634,6 @@ int gather_root(fcx_dist *d, fcx_ctx *c, const uint8_t *d_in, uint64_t n, const 
     std::string own_msg = own_rc ? fcx_last_error() : "";
     std::vector<uint64_t> fill(N, 0);
     std::string peer_err;
-    bool broken = false;   // a peer announced a piece beyond its bound: the protocol cannot continue
     for (uint32_t s = 0; s < nsub && N > 1; s++) {
         uint64_t *ws = dw + 2ull * s * N, *hs = hw + 2ull * s * N;
         DTRY(t.group_start());
@@ -638,6 +644,22 @@ int gather_root(fcx_dist *d, fcx_ctx *c, const uint8_t *d_in, uint64_t n, const 
         DTRY(rc2);
         DHIP(hipMemcpyAsync(hs, ws, 2ull * N * sizeof(uint64_t), hipMemcpyDeviceToHost, d->cst));
         DHIP(hipStreamSynchronize(d->cst));
+        // a piece beyond its peer's staging bound (the ranks disagree on rank_bytes; a peer checks
+        // its pieces against the same bound otherwise) is still received -- into the drain buffer,
+        // so the peer's send completes and the protocol runs on to the failing verdict
+        uint64_t drain = 0;
+        for (int r = 1; r < N; r++) {
+            const uint64_t len = hs[2 * r], err = hs[2 * r + 1];
+            if (!err && len != kFailed && len && fill[r] + len > bound[r]) drain = std::max(drain, len);
+        }
+        if (drain > d->drain_cap) {
+            if (d->d_drain) DHIP(hipFree(d->d_drain));
+            d->d_drain = nullptr;
+            d->drain_cap = 0;
+            if (hipMalloc((void **)&d->d_drain, drain) != hipSuccess)
+                return dfail(FCX_ERR_NOMEM, "fcx_dist_compress_gather: drain buffer of " + std::to_string(drain) + " B");
+            d->drain_cap = drain;
+        }
         DTRY(t.group_start());
         for (int r = 1; r < N && !rc; r++) {
             const uint64_t len = hs[2 * r], err = hs[2 * r + 1];
@@ -646,9 +668,9 @@ int gather_root(fcx_dist *d, fcx_ctx *c, const uint8_t *d_in, uint64_t n, const 
                 continue;
             }
             if (len == 0) continue;
-            if (fill[r] + len > bound[r]) {   // (a peer checks its pieces against the same bound)
-                broken = true;
+            if (fill[r] + len > bound[r]) {
                 if (peer_err.empty()) peer_err = "rank " + std::to_string(r) + " sent a piece beyond its bound";
+                rc = t.recv(d->d_drain, len, r, d->cst);   // (concurrent drains of one round share it: dropped)
                 continue;
             }
             rc = t.recv(d->d_stage + soff[r] + fill[r], len, r, d->cst);
@@ -657,10 +679,6 @@ int gather_root(fcx_dist *d, fcx_ctx *c, const uint8_t *d_in, uint64_t n, const 
         const int rc3 = t.group_end();
         DTRY(rc);
         DTRY(rc3);
-        if (broken) {   // the peer is blocked in a send nobody receives: release it with an error
-            t.abort();
-            return dfail(FCX_ERR_INTERNAL, "fcx_dist_compress_gather: " + peer_err);
-        }
     }
     DHIP(hipStreamSynchronize(d->cst));
     uint64_t own = 0;

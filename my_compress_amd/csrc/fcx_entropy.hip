@@ -138,7 +138,6 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / kStreams, s = blockIdx.x % kStreams;
     BlockInfo &bi = binfo[b];
-    if (s == 1 && tid == 0) atomicAdd(err + 3, 1u);   // (blocks of the call: the small-alphabet share below)
     if (!stream_active(bi, s)) {
         if (tid == 0) { bi.hdrlen[s] = 0; bi.nwords[s] = 0; }
         return;
@@ -231,16 +230,6 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
 #pragma unroll
     for (uint32_t u = 0; u < 256 / kTreeT; u++) nz += w[tid + kTreeT * u] != 0 ? 1u : 0u;
     const uint32_t real = (uint32_t)__syncthreads_count(nz >= 1) + (uint32_t)__syncthreads_count(nz >= 2);
-    // small-alphabet block (<= 6 literal symbols, short matches: dense 3-byte keys), match-dense
-    // block (>= 1 match per 32 bytes: text), long-match block (<= 1 token per 16 bytes: runs,
-    // zeros) and few-match block (>= 1 token per 2 bytes, < 1 match per 1024: random data), counted
-    // for the context's choice of the match kernel in later calls (fcx_capi.hip)
-    if (s == 1 && tid == 0 && bi.len >= 65536) {
-        if (real <= 6 && bi.ntok >= bi.len / 32) atomicAdd(err + 2, 1u);
-        if (32 * (uint64_t)bi.nmatch >= bi.len) atomicAdd(err + 4, 1u);
-        if (16 * (uint64_t)bi.ntok <= bi.len) atomicAdd(err + 5, 1u);
-        if (2 * (uint64_t)bi.ntok >= bi.len && 1024 * (uint64_t)bi.nmatch < bi.len) atomicAdd(err + 6, 1u);
-    }
     // stable sort of the leaves by (weight, symbol): rank = number of smaller keys.  A weight is at
     // most the block size (<= 2^20 symbols), so weight << 8 | symbol fits 32 bits
 #pragma unroll

@@ -83,6 +83,12 @@
 #ifndef FCX_NOBUCKET
 #define FCX_NOBUCKET FCX_SPARSE
 #endif
+// FCX_REST (fcx_match_rest.hip): the general kernel's tile body in k_match_rest, the loop over the
+// tiles a routed call's unit launches did not cover (fcx_route.hip).  Its own translation unit, so
+// the general k_match keeps its code generation.
+#ifndef FCX_REST
+#define FCX_REST 0
+#endif
 #if FCX_SPARSE   // (the sparse search inline in its own unit: rand k_match 2.43 -> 2.31 ms per GiB)
 #define FCX_SPARSE_CALL __forceinline__
 #else
@@ -821,14 +827,16 @@ __device__ inline uint32_t xcd_tile(uint32_t w, uint32_t n) {
     return x * q + min(x, r) + j;
 }
 
+// One tile bx of the shard, by the whole workgroup (every return is workgroup-uniform).
 // kDev = false is the product kernel: every development / test-mode bit is compiled out.
 // k_match<true> carries them (phase exits for tools/matchphase.py through fcx_debug_match, and
 // the forced tile modes of fcx_ctx_set_match_mode, which the parity tests use).
 template <bool kDev>
-__global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
-                                              uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
-                                              uint64_t *__restrict__ chain_pfx,
-                                              uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg_in) {
+__device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const Layout L, uint32_t *__restrict__ m,
+                                           uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
+                                           uint64_t *__restrict__ chain_pfx, uint32_t *__restrict__ tinfo,
+                                           uint32_t *__restrict__ mtok, uint32_t dbg_in, const uint32_t bx,
+                                           const MatchRoute &rt) {
     const uint32_t dbg = kDev ? dbg_in : (uint32_t)FCX_MATCH_EXIT;   // (FCX_MATCH_EXIT: phase-timing builds only)
     __shared__ __attribute__((aligned(16))) uint32_t sdw[kTileBytes / 4 + 4];   // byte image of the window
     // one region, two lives: [bucket counters/starts (u16 x 4104) | entries (u16 x 6144)] during the
@@ -855,7 +863,6 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     __shared__ uint32_t s_red[4 * kWaves];   // cross-wave scan partials (rmode_walk: exits + 3 scans)
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t bx = xcd_tile(blockIdx.x, gridDim.x);   // this workgroup's tile
     const uint32_t b = bx / L.tpb, k = bx % L.tpb;
     const uint64_t bstart = (uint64_t)b * L.B;
     const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
@@ -915,6 +922,9 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         for (uint32_t x = tid; x < kFilterWords / 4; x += kMT) r4[x] = make_uint4(0u, 0u, 0u, 0u);
     }
 #endif
+    // a direct routed launch (every tile in the grid): another unit's tile ends here, its kind read
+    // while the staging loads were in flight; nothing but this workgroup's LDS was written
+    if (!rt.list && rt.kind && rt.kind[bx] != rt.mine) return;
     __syncthreads();
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
@@ -1048,6 +1058,15 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         __syncthreads();
         if (dbg & 32u) return;
 #if FCX_NOBUCKET
+    } else if (rt.defer_list) {
+        // not sparse, in a routed call: the tile goes on to the no-filter unit's list (launched after
+        // this one), which searches it by buckets.  Nothing of it has been written yet.  (The run
+        // table below overflows on match-dense tiles and leaves them to the stitch's serial walk.)
+        if (tid == 0) {
+            rt.defer_list[atomicAdd(rt.defer_cnt, 1u)] = bx;
+            rt.kind[bx] = (uint8_t)kRouteNoFilter;   // (a direct no-filter launch finds it by its kind)
+        }
+        return;
     } else {   // not sparse: the whole-tile run-table mode, as for run-mode tiles
         rmode = true;
         for (uint32_t x = tid; x < kTile; x += kMT) step[x] = 0;
@@ -1580,19 +1599,80 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
 }
 
+// The unit's kernel: one workgroup per tile.  Unrouted (rt.list null: forced units, development)
+// the grid is every tile of the shard; routed (fcx_route.hip) the grid is a host estimate of the
+// unit's list and workgroup i takes list entry i, if there is one (the entries past the grid go to
+// k_match_rest).  Either way each XCD takes a contiguous run of entries (xcd_tile).
+#if !FCX_REST
+template <bool kDev>
+__global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
+                                              uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
+                                              uint64_t *__restrict__ chain_pfx,
+                                              uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg_in,
+                                              MatchRoute rt) {
+    uint32_t bx = xcd_tile(blockIdx.x, gridDim.x);
+    if (rt.list) {   // (both loads in flight together: the grid never exceeds the list's storage)
+        const uint32_t c = *rt.cnt, t = rt.list[bx];
+        if (bx >= c) return;
+        bx = t;
+    }
+    match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rt);
+}
+#endif
+
+#if FCX_REST
+// The routed call's remainder, by the general kernel: the entries of each unit's list past the
+// grid the host gave that unit (rest.grid[u]; a unit not launched has grid 0), i.e. the tiles of
+// kinds the host did not expect.  A fixed grid of workgroups loops over them (the count is only
+// known on the device); with none left every workgroup exits at once.
+__global__ __launch_bounds__(kMT, 8) void k_match_rest(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
+                                                   uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
+                                                   uint64_t *__restrict__ chain_pfx, uint32_t *__restrict__ tinfo,
+                                                   uint32_t *__restrict__ mtok, RouteRest rest) {
+    uint32_t left[kRoutes], total = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kRoutes; u++) {
+        const uint32_t c = rest.cnt[u];
+        left[u] = c > rest.grid[u] ? c - rest.grid[u] : 0u;
+        total += left[u];
+    }
+    const MatchRoute none{};
+    for (uint32_t i = blockIdx.x; i < total; i += gridDim.x) {
+        uint32_t u = 0, p = i;
+        while (u + 1 < kRoutes && p >= left[u]) { p -= left[u]; u++; }
+        const uint32_t bx = rest.lists[(uint64_t)u * rest.list_stride + rest.grid[u] + p];
+        match_tile<false>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u, bx, none);
+        __syncthreads();   // the next tile's staging overwrites the LDS this one read
+    }
+}
+
+void launch_match_rest(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                       uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, const RouteRest &rest, uint32_t grid,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_match_rest, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, rest);
+}
+#endif
+
+#if !FCX_REST
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
-                  uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override) {
+                  uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override, const MatchRoute *route,
+                  uint32_t grid_override) {
     // dbg bits (k_match<true> only): fcx_debug_match's phase exits and experiment bits
     // (development; the kernel alone on scratch the caller discards) and the forced tile modes
     // of fcx_ctx_set_match_mode (bit2 never / bit3 always the whole-tile run mode, bit7 no
     // repeat filter; output unchanged).  The default path launches k_match<false>, compiled
     // without any of them; nothing is read from the environment.
     const uint32_t dbg = dbg_override != ~0u ? dbg_override : 0u;
-    const uint32_t grid = L.nblocks * L.tpb;
+    const MatchRoute rt = route ? *route : MatchRoute{};
+    const uint32_t grid = rt.list ? grid_override : L.nblocks * L.tpb;
+    if (grid == 0) return;
     if (dbg == 0)
-        hipLaunchKernelGGL(k_match<false>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u);
+        hipLaunchKernelGGL(k_match<false>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u,
+                           rt);
     else
-        hipLaunchKernelGGL(k_match<true>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg);
+        hipLaunchKernelGGL(k_match<true>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg,
+                           rt);
 }
+#endif
 
 }  // namespace fcx

@@ -58,9 +58,9 @@ def piece_ranges(n: int, block_bytes: int, nsub: int):
 
 # ---- the strong-scaling step model --------------------------------------------
 # One GPU's compress time per GiB and output ratio for each synthetic kind at 1 MiB blocks
-# (bench.py on one MI355X, profiles/r04_bench_n1.json), the defaults of gather_share_ppm.
-COMPRESS_MS_PER_GIB = {"rand": 4.54, "text": 14.06, "zeros": 3.33, "runs": 11.92, "dna": 57.85}
-RATIO = {"rand": 1.0164, "text": 0.582, "zeros": 0.007, "runs": 0.0396, "dna": 0.27}
+# (bench.py on one MI355X, profiles/r06_bench_n1.json), the defaults of gather_share_ppm.
+COMPRESS_MS_PER_GIB = {"rand": 4.30, "text": 13.0, "zeros": 2.70, "runs": 11.9, "dna": 28.0, "mix": 14.0}
+RATIO = {"rand": 1.0163, "text": 0.5805, "zeros": 0.0070, "runs": 0.0396, "dna": 0.3112, "mix": 0.487}
 
 
 def step_model_ms(share0: float, world: int, c_ms: float, ratio: float, link_gbps: float, nsub: int,
@@ -179,7 +179,7 @@ def allgather_segments(seg: torch.Tensor, out: torch.Tensor, sizes, offs, dist, 
 
 
 def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=None, out=None, group=None,
-                    device=None):
+                    device=None, own_error=None):
     """fcx_dist_compress_gather's protocol over torch.distributed (the `--concat-impl torch` path
     and the gloo tests).  A peer passes `pieces`, an iterable of its nsub sub-batch segments in
     order (uint8 tensors, e.g. compressed one by one as they are consumed): each is sent as it is
@@ -188,7 +188,9 @@ def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=N
     concatenation); per round s it receives every peer's length pair, then every peer's bytes
     into a staging region per peer, and finally moves them behind its own segment in rank order.
     A peer that fails sends (-1, 1) for this and every later round.  Rank 0 then sends the job's
-    verdict (0 or 1) to every peer, so every rank raises when any rank failed.  `device`: where a
+    verdict (0 or 1) to every peer, so every rank raises when any rank failed -- a peer's failure,
+    a piece beyond its peer's staging bound (drained, not stored), rank 0's own failure
+    (`own_error`, a message) or an `out` too small for the whole concatenation.  `device`: where a
     peer's control words live (its pieces' device; required under nccl, which cannot send CPU
     tensors).  Returns the concatenated length on rank 0, the bytes sent on a peer."""
     rank = dist.get_rank(group)
@@ -234,12 +236,20 @@ def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=N
             if e or n < 0:
                 err = err or f"rank {r} failed in sub-batch {s}"
                 continue
-            if n:
+            if n and fill[r] + n > stage_cap[r]:   # beyond the peer's bound: drained, the job fails
+                err = err or f"rank {r} sent a piece beyond its bound in sub-batch {s}"
+                ops.append(dist.P2POp(dist.irecv, torch.empty(n, dtype=torch.uint8, device=dev), r, group))
+            elif n:
                 ops.append(dist.P2POp(dist.irecv, stage[r][fill[r]:fill[r] + n], r, group))
                 fill[r] += n
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+    n_own = int(own.numel()) if own is not None else 0
+    if not err and own_error:
+        err = f"rank 0 failed: {own_error}"
+    if not err and (out is None or n_own + sum(fill) > out.numel()):
+        err = f"output capacity too small ({n_own + sum(fill)} B)"
     verdict = torch.tensor([1 if err else 0], dtype=torch.int64, device=dev)
     ops = [dist.P2POp(dist.isend, verdict, r, group) for r in range(1, world)]
     if ops:
@@ -247,7 +257,6 @@ def compress_gather(pieces, dist, rank_bytes, block_bytes: int, nsub: int, own=N
             w.wait()
     if err:
         raise RuntimeError("compress_gather: " + err)
-    n_own = int(own.numel()) if own is not None else 0
     _place_own(own if own is not None else torch.zeros(0, dtype=torch.uint8, device=dev), out, 0)
     off = n_own
     for r in range(1, world):

@@ -28,15 +28,38 @@ def gen_lib():
     return _gen
 
 
+# the `mix` input (bench leg `mix`): 1 MiB blocks cycling through four kinds -- block i is block
+# i // 4 of the stream MIX_STREAMS[i % 4] (the same streams and seeds as the per-kind bench legs)
+MIX_STREAMS = (("rand", 4), ("text", 3), ("runs", 5), ("dna", 6))
+MIX_BLOCK = MiB
+
+
+def mix_into(ptr: int, n: int) -> None:
+    nb = (n + MIX_BLOCK - 1) // MIX_BLOCK
+    for k, (kind, seed) in enumerate(MIX_STREAMS):
+        mine = range(k, nb, len(MIX_STREAMS))
+        if not len(mine):
+            continue
+        tmp = ctypes.create_string_buffer(len(mine) * MIX_BLOCK)
+        gen_lib().fcxgen_generate(GEN_KIND[kind], seed, tmp, len(mine) * MIX_BLOCK)
+        for j, i in enumerate(mine):
+            ln = min(MIX_BLOCK, n - i * MIX_BLOCK)
+            ctypes.memmove(ptr + i * MIX_BLOCK, ctypes.addressof(tmp) + j * MIX_BLOCK, ln)
+
+
 def generate(kind: str, seed: int, n: int) -> bytes:
     buf = ctypes.create_string_buffer(max(n, 1))
-    gen_lib().fcxgen_generate(GEN_KIND[kind], seed, buf, n)
+    generate_into(kind, seed, ctypes.addressof(buf), n)
     return buf.raw[:n]
 
 
 def generate_into(kind: str, seed: int, ptr: int, n: int) -> None:
-    """fill host memory at `ptr` (e.g. a pinned torch tensor) with n bytes"""
-    gen_lib().fcxgen_generate(GEN_KIND[kind], seed, ctypes.c_void_p(ptr), n)
+    """fill host memory at `ptr` (e.g. a pinned torch tensor) with n bytes (kind "mix": mix_into,
+    the seed is unused)"""
+    if kind == "mix":
+        mix_into(ptr, n)
+    else:
+        gen_lib().fcxgen_generate(GEN_KIND[kind], seed, ctypes.c_void_p(ptr), n)
 
 
 def _lcg(seed):
@@ -164,6 +187,11 @@ SURVEY_DIGESTS = {
     "cfg5b_runs_1GiB": {"kind": "runs", "seed": 5, "n": 1024 * MiB, "block": MiB,
                         "in": "18cddd87a89e44af896056a31ae955c56deea5bf47ab1de5ab491796d5115ef3",
                         "bytes": 42548682, "out": "4fced94fd4725ba3b1031dec67d63e1295b95ae08cc1cf0e34c84769f5313d26"},
+    # not a SURVEY digest: the bench's `mix` leg, made here by the reference compiled in place
+    # (tests/golden/make_mix_digest.py)
+    "mix_1GiB": {"kind": "mix", "seed": 0, "n": 1024 * MiB, "block": MiB,
+                 "in": "02afe5c4c67cbf572024632afed721e1d90bb58f44b40259422cb3fd23db3ae2",
+                 "bytes": 523200760, "out": "ce8bb8bc756a62fcd276d6a71b93456c18a7def3d77e555ea7eb8b92bfebffb5"},
     "hl_text_1GiB": {"kind": "text", "seed": 3, "n": 1024 * MiB, "block": MiB,
                      "in": "713e4aa36f5d3604cc756c4abf995bc0355d1c7387379c60bcd24b8556c3bdea",
                      "bytes": 624801500, "out": "132a36b9d2592f8c37a82b51f545ddb67acec53fa1a31b7f1f6a04617a01a3d1"},

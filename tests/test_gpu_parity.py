@@ -247,7 +247,7 @@ def test_cfg2_64MiB_rand_64KiB_digest(gpu_compress):
 
 @pytest.mark.slow
 @pytest.mark.parametrize("name", ["hl_text_1GiB", "hl_rand_1GiB", "cfg3_text_1GiB", "cfg5a_zeros_1GiB",
-                                  "cfg5b_runs_1GiB"])
+                                  "cfg5b_runs_1GiB", "mix_1GiB"])
 def test_full_size_digests(name, cuda):
     import torch
 
@@ -329,10 +329,9 @@ def _small_alphabet_mix(seed: int, n: int) -> bytes:
 
 @pytest.mark.parametrize("block", [1 << 20, 65536, 5000])
 def test_key4_kernel_vs_oracle(cuda, block):
-    """the 4-byte-key match kernel (fcx_match_k4.hip): forced (mode 4) and chosen by the
-    context from its previous call (mode 0: 'ACGT' data switches from the second call on),
-    against the oracle on dna, mixed small-alphabet / text / random / periodic data and a
-    ragged tail"""
+    """the 4-byte-key match unit (fcx_match_k4.hip): forced (mode 4) and routed (mode 0: 'ACGT'
+    tiles go to it from the first call on), against the oracle on dna, mixed small-alphabet /
+    text / random / periodic data and a ragged tail"""
     import torch
 
     kernel = mc.lib().fcx_ctx_match_kernel
@@ -355,25 +354,27 @@ def test_key4_kernel_vs_oracle(cuda, block):
                     assert got == want, (name, block, mode, call)
                     if mode == 4:
                         assert kernel(ctx._h) == 1
-                    elif name == "dna" and block >= 65536:
-                        assert kernel(ctx._h) == (0 if call == 0 else 1), (block, call)
+                    elif name == "dna":
+                        assert kernel(ctx._h) == 1, (name, block, call)
+                        rs = ctx.route_stats()
+                        assert rs["key4"] >= rs["tiles"] - 1 and rs["rest"] == 0, (name, block, call, rs)
             finally:
                 ctx.close()
 
 
 @pytest.mark.parametrize("block", [1 << 20, 262144])
-def test_match_dense_kernel_auto(cuda, block):
-    """match-dense shards (text) switch to the kernel without the repeat filter from the
-    second call on, long-match shards (runs, zeros) to the runs kernel, random data to the
-    kernel without the bucket search; the bytes equal the oracle's"""
+def test_match_units_routed(cuda, block):
+    """text tiles go to the unit without the repeat filter, long-match tiles (runs, zeros) to the
+    runs unit, random data to the unit without the bucket search -- from a context's first call,
+    decided by each tile's own bytes; the bytes equal the oracle's"""
     import torch
 
     kernel = mc.lib().fcx_ctx_match_kernel
-    for name, data, want_kernel in (("text", inputs.generate("text", 3, 3 << 20), 2),
-                                    ("rand", inputs.generate("rand", 4, 3 << 20), 4),
-                                    ("runs", inputs.generate("runs", 5, 3 << 20), 3),
-                                    ("zeros", bytes(3 << 20), 3),
-                                    ("mix", _small_alphabet_mix(9, 2 << 20), None)):
+    for name, data, want_kernel, lst in (("text", inputs.generate("text", 3, 3 << 20), 2, "nofilter"),
+                                         ("rand", inputs.generate("rand", 4, 3 << 20), 4, "sparse"),
+                                         ("runs", inputs.generate("runs", 5, 3 << 20), 3, "runs"),
+                                         ("zeros", bytes(3 << 20), 3, "runs"),
+                                         ("mix", _small_alphabet_mix(9, 2 << 20), None, None)):
         want = oracle.compress_file(data, block)
         d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
         cap = mc.shard_bound(len(data), block)
@@ -386,7 +387,12 @@ def test_match_dense_kernel_auto(cuda, block):
                                        torch.cuda.current_stream().cuda_stream)
                 got = mc.write_header(len(data), nb) + d_out[:n].cpu().numpy().tobytes()
                 assert got == want, (name, block, call)
+                rs = ctx.route_stats()
+                assert rs["cold"] == (1 if call == 0 else 0), (name, call, rs)
+                assert rs["tiles"] == sum((min(block, len(data) - b0) + 4095) // 4096
+                                          for b0 in range(0, len(data), block)), rs
                 if want_kernel is not None:
-                    assert kernel(ctx._h) == (0 if call == 0 else want_kernel), (name, block, call)
+                    assert kernel(ctx._h) == want_kernel, (name, block, call)
+                    assert rs[lst] == rs["tiles"] and rs["rest"] == 0 and rs["handed_on"] == 0, (name, call, rs)
         finally:
             ctx.close()

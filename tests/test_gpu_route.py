@@ -1,0 +1,146 @@
+"""Per-tile routing of the match search (fcx_route.hip): the unit that searches a tile is chosen
+from that tile's own bytes in the same call, so the bytes -- and the speed -- do not depend on
+what a context compressed before.  The reference's block codec carries no state between blocks
+(my_compress.cpp:4090-4122; parse 1675-1714).  Bar: bit-exact against the oracle / the
+reference's digests; the route statistics show which unit took which tiles.
+"""
+import hashlib
+import io
+import random
+
+import pytest
+
+import inputs
+import my_compress_amd as mc
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("rand", "text", "runs", "dna")
+
+
+def mixed_blocks(seed: int, nblocks: int, block: int) -> bytes:
+    """blocks cycling rand / text / runs / dna (the bench's `mix` leg at a smaller size)"""
+    return b"".join(inputs.generate(KINDS[i % 4], seed + i, block) for i in range(nblocks))
+
+
+def _compress(ctx, cuda, data: bytes, block: int) -> bytes:
+    import torch
+
+    d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
+    cap = mc.shard_bound(len(data), block)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=cuda)
+    n = ctx.compress_shard(d_in.data_ptr(), len(data), d_out.data_ptr(), cap, torch.cuda.current_stream().cuda_stream)
+    return mc.write_header(len(data), (len(data) + block - 1) // block) + d_out[:n].cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("block", [1 << 20, 262144, 65536])
+def test_mixed_blocks_every_unit(cuda, block):
+    """one shard whose blocks cycle through four kinds: each kind's tiles go to its own unit in
+    the same call, nothing is left to k_match_rest in steady state, and the bytes are exact"""
+    data = mixed_blocks(11, 8, 1 << 20)
+    want = oracle.compress_file(data, block)
+    ctx = mc.Context(0, block, len(data))
+    try:
+        for call in range(3):
+            assert _compress(ctx, cuda, data, block) == want, (block, call)
+            rs = ctx.route_stats()
+            q = rs["tiles"] // 4
+            assert rs["tiles"] == len(data) // 4096
+            # each kind is a quarter of the tiles (a few first-tiles of text blocks may file as sparse)
+            assert abs(rs["sparse"] - q) <= 8 and rs["runs"] == q and rs["key4"] == q, rs
+            assert rs["sparse"] + rs["runs"] + rs["key4"] + rs["nofilter"] - rs["handed_on"] == rs["tiles"], rs
+            assert rs["cold"] == (call == 0), rs
+            if call > 0:
+                assert rs["rest"] == 0, rs
+    finally:
+        ctx.close()
+
+
+def test_kind_changes_between_calls(cuda):
+    """one context, consecutive calls of different kinds: the first tiles of a kind the estimate
+    did not foresee are searched by k_match_rest (the general kernel), and the bytes stay exact;
+    the call after sizes the new kind's unit from the new counts"""
+    block = 1 << 20
+    ctx = mc.Context(0, block, 4 << 20)
+    try:
+        seen_rest = 0
+        for i, kind in enumerate(["rand", "text", "text", "runs", "dna", "zeros", "rand", "text"]):
+            data = bytes(4 << 20) if kind == "zeros" else inputs.generate(kind, 40 + i, 4 << 20)
+            got = _compress(ctx, cuda, data, block)
+            assert got == oracle.compress_file(data, block), (i, kind)
+            rs = ctx.route_stats()
+            seen_rest += rs["rest"]
+            assert rs["cold"] == (i == 0)
+        assert seen_rest > 0   # the change of kind was absorbed by k_match_rest, not by a stale unit
+    finally:
+        ctx.close()
+
+
+def test_misfiled_tiles_handed_on(cuda):
+    """tiles whose sample looks random (all 256 byte values) but which repeat within the window:
+    the classifier files them for the sparse unit, whose repeat filter refuses them; they are
+    handed on to the no-filter unit (never to the whole-tile run table) and the bytes are exact"""
+    rng = random.Random(5)
+    perm = list(range(256))
+    parts = []
+    for _ in range(64):
+        rng.shuffle(perm)
+        unit = bytes(perm)
+        parts.append(unit * 8 + inputs.generate("text", rng.randrange(1 << 20), 2048))
+    data = b"".join(parts)
+    block = 1 << 20
+    ctx = mc.Context(0, block, len(data))
+    try:
+        for call in range(2):
+            assert _compress(ctx, cuda, data, block) == oracle.compress_file(data, block)
+            rs = ctx.route_stats()
+            assert rs["handed_on"] > 0, rs
+            st = ctx.stats()
+            assert st["lazy_tiles"] == 0, st
+    finally:
+        ctx.close()
+
+
+def test_forced_unit_is_unrouted(cuda):
+    """a forced unit (fcx_ctx_set_match_mode 4-7) runs unrouted over every tile: no route stats"""
+    data = inputs.generate("text", 2, 1 << 20)
+    ctx = mc.Context(0, 1 << 20, len(data))
+    try:
+        ctx.set_match_mode(7)
+        assert _compress(ctx, cuda, data, 1 << 20) == oracle.compress_file(data, 1 << 20)
+        with pytest.raises(mc.FcxError):
+            ctx.route_stats()
+        ctx.set_match_mode(0)
+        assert _compress(ctx, cuda, data, 1 << 20) == oracle.compress_file(data, 1 << 20)
+        assert ctx.route_stats()["nofilter"] == 256
+    finally:
+        ctx.close()
+
+
+def test_stream_across_kinds(cuda):
+    """the stream path (fcx_compress_stream) on one context over rand, then text, then runs, in
+    shards smaller than each part: every shard is routed from its own bytes; the records equal
+    the per-part records (independent blocks), and each part is the reference's / oracle's"""
+    block = 1 << 20
+    parts = [inputs.generate(k, 60 + i, 24 << 20) for i, k in enumerate(["rand", "text", "runs"])]
+    data = b"".join(parts)
+    ctx = mc.Context(0, block, 8 << 20)
+    try:
+        src, sink = io.BytesIO(data), io.BytesIO()
+        tin, tout, nb = ctx.compress_stream(src, sink, 8 << 20)
+        assert (tin, nb) == (len(data), len(data) // block)
+        recs = sink.getvalue()
+        assert len(recs) == tout
+    finally:
+        ctx.close()
+    want = b""
+    for p in parts:   # the part's records, from a fresh context (cold, routed from its own counts)
+        c = mc.Context(0, block, len(p))
+        try:
+            want += _compress(c, cuda, p, block)[10:]
+        finally:
+            c.close()
+    assert hashlib.sha256(recs).hexdigest() == hashlib.sha256(want).hexdigest()
+    small = parts[1][: 2 << 20]
+    assert _compress(mc.Context(0, block, len(small)), cuda, small, block) == oracle.compress_file(small, block)

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check", default=None)
     ap.add_argument("--groups", default="0", help="comma list of fcx_ctx_set_groups values to time")
+    ap.add_argument("--mode", type=int, default=0, help="fcx_ctx_set_match_mode (0: routed)")
     a = ap.parse_args()
     n = a.mib << 20
     t = time.time()
@@ -41,6 +42,7 @@ def main():
     cap = mc.shard_bound(n, a.block)
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     ctx = mc.Context(0, a.block, n)
+    ctx.set_match_mode(a.mode)
     st = torch.cuda.current_stream().cuda_stream
     got = ctx.compress_shard(d_in.data_ptr(), n, d_out.data_ptr(), cap, st)  # warm
     for G in [int(x) for x in a.groups.split(",")]:
@@ -66,6 +68,10 @@ def main():
             print("   digest", "OK" if h.hexdigest() == cfg["out"] and got + 10 == cfg["bytes"] else "MISMATCH",
                   got + 10, cfg["bytes"], flush=True)
     print(ctx.stats())
+    try:
+        print("route", ctx.route_stats())
+    except (mc.FcxError, AttributeError):
+        pass
     ctx.close()
 
 
