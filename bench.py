@@ -468,8 +468,13 @@ def transition_leg(dev, block=1 << 20, shard_mib=256, calls=4):
     ins = {k: make_input(k, SEEDS[k], 0, n).to(dev) for k in ("rand", "text")}
     cap = mc.shard_bound(n, block)
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
-    ctx = mc.Context(dev.index, block, n)
     sid = torch.cuda.current_stream(dev).cuda_stream
+    warm = make_input("mix", 0, 0, 64 << 20).to(dev)   # every match kernel's code loaded before timing
+    w = mc.Context(dev.index, block, warm.numel())
+    w.compress_shard(warm.data_ptr(), warm.numel(), d_out.data_ptr(), cap, sid)
+    w.close()
+    del warm
+    ctx = mc.Context(dev.index, block, n)
     ms, rest = {"rand": [], "text": []}, []
     try:
         for k in ("rand", "text"):

@@ -107,7 +107,7 @@ using MatchLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64
 constexpr int kRouteKernel[kRoutes] = {kMatchSparse, kMatchRuns, kMatchKey4, kMatchNoFilter};
 constexpr uint32_t kRouteWords = 8;         // device counters per block group (k_classify: cnt[0..5])
 constexpr uint32_t kRouteMinTiles = 8;      // a unit expected to get fewer tiles is not launched (k_match_rest)
-constexpr uint32_t kRestGrid = 1024;        // k_match_rest's workgroups (4 per CU)
+constexpr uint32_t kRestGrid = 512;         // k_match_rest's workgroups (2 per CU: 128 VGPRs)
 constexpr uint64_t kRouteBytes = 4ull * kRouteWords * 8;   // route counters of kMaxGroups (= 8) groups
 constexpr uint64_t kWordBytes = 64 + kRouteBytes;          // dev_words
 static MatchLaunch match_launcher(int k) {

@@ -83,11 +83,19 @@
 #ifndef FCX_NOBUCKET
 #define FCX_NOBUCKET FCX_SPARSE
 #endif
+// FCX_SHORTK (the no-filter unit): waves whose longest bucket range is at most this many entries skip
+// the K search and pass B of the bucket scan (0: never)
+#ifndef FCX_SHORTK
+#define FCX_SHORTK 0
+#endif
 // FCX_REST (fcx_match_rest.hip): the general kernel's tile body in k_match_rest, the loop over the
 // tiles a routed call's unit launches did not cover (fcx_route.hip).  Its own translation unit, so
 // the general k_match keeps its code generation.
 #ifndef FCX_REST
 #define FCX_REST 0
+#endif
+#ifndef FCX_REST_WAVES
+#define FCX_REST_WAVES 8
 #endif
 #if FCX_SPARSE   // (the sparse search inline in its own unit: rand k_match 2.43 -> 2.31 ms per GiB)
 #define FCX_SPARSE_CALL __forceinline__
@@ -121,6 +129,19 @@
 #endif
 
 namespace fcx {
+
+#if FCX_REST
+// k_match_rest loops over tiles: the thread index is re-read per use through an opaque asm, so
+// nothing derived from it is hoisted out of the loop and kept live across a whole tile body
+__device__ inline uint32_t rest_tid() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+#define FCX_TID rest_tid()
+#else
+#define FCX_TID threadIdx.x
+#endif
 
 constexpr uint32_t kWinPos = kHalo + 1 + kTile;      // 6144 window positions per tile
 constexpr uint32_t kMT = kMatchThreads;              // 512
@@ -193,7 +214,7 @@ __device__ __attribute__((always_inline)) inline void dense_phase_body(const uin
     const uint32_t dbg = kDev ? uni(dbg_in) : 0u;   // development bits exist only in k_match<true>
     q0 = uni(q0); npos = uni(npos); nload = uni(nload); ilen = uni(ilen); w0 = uni(w0);   // (arguments arrive
     rt_cap = uni(rt_cap);                                                                 //  in VGPRs)
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = FCX_TID;
     uint32_t *rbm = region + kTile / 2;                       // boundary bitmap, kRunBmWords
     uint16_t *prc = (uint16_t *)(rbm + kRunBmWords);          // prefix counts per bitmap word
     uint32_t *rt = rbm + kRunBmWords + kRunBmWords / 2 + 2 + kRunListWords;   // run table
@@ -404,7 +425,7 @@ __device__ inline uint32_t rm_stepat(FCX_LDS uint32_t *region, uint32_t x, uint3
 __device__ FCX_RMODE_CALL void rmode_walk(FCX_LDS uint32_t *region, FCX_LDS uint32_t *s_ex, FCX_LDS uint32_t *s_unknown,
                                         uint32_t q0, uint32_t nt, uint32_t ilen, uint32_t w0, uint32_t t0, uint64_t *mbw,
                                         uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t *mt, uint32_t dbg) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);   // walks: wave-uniform, scalar
+    const uint32_t tid = FCX_TID, lane = tid & 63, wv = uni(tid >> 6);   // walks: wave-uniform, scalar
     q0 = uni(q0); nt = uni(nt); ilen = uni(ilen); w0 = uni(w0); t0 = uni(t0);   // (arguments arrive in VGPRs)
     FCX_LDS uint16_t *step = (FCX_LDS uint16_t *)region;
     FCX_LDS uint16_t *dist = (FCX_LDS uint16_t *)(region + kRmDist);
@@ -563,7 +584,7 @@ __device__ FCX_SPARSE_CALL void sparse_search(const uint32_t *sdw, uint32_t *reg
                                            uint32_t blen, uint32_t ntile, uint32_t dbg_in) {
     const uint32_t dbg = kDev ? uni(dbg_in) : 0u;
     q0 = uni(q0); npos = uni(npos); ins_end = uni(ins_end); w0 = uni(w0); blen = uni(blen); ntile = uni(ntile);
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = FCX_TID;
     const uint32_t kw[4] = {kw0, kw1, kw2, kw3};
     auto hash_of = [&](uint32_t r) -> uint32_t {
         return key_mix(__builtin_amdgcn_alignbyte(kw[(r >> 2) + 1], kw[r >> 2], r & 3) & 0xFFFFFFu);
@@ -672,14 +693,14 @@ __device__ FCX_SPARSE_CALL void sparse_search(const uint32_t *sdw, uint32_t *reg
 // written) above 64 match positions; every wave returns the same verdict.
 __device__ inline bool sparse_parse(const uint64_t *mbl, const uint16_t *step, const uint32_t *res, uint32_t *list,
                                     uint32_t nt, uint32_t t0, uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t *mt) {
-    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane = FCX_TID & 63;
     const uint32_t nwords = (nt + 63) / 64;
     const uint64_t wm = lane < nwords ? mbl[lane] : 0ull;
     const uint32_t cntw = (uint32_t)__popcll(wm);
     const uint32_t inc = wave_incl_scan(cntw);
     const uint32_t nm = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     if (nm > 64) return false;
-    if (threadIdx.x >= 64) return true;
+    if (FCX_TID >= 64) return true;
     uint32_t k = inc - cntw;
     for (uint64_t bits = wm; bits; bits &= bits - 1, k++) list[k] = 64 * lane + (uint32_t)__builtin_ctzll(bits);
     __builtin_amdgcn_wave_barrier();
@@ -738,7 +759,7 @@ __device__ inline bool sparse_parse(const uint64_t *mbl, const uint16_t *step, c
 __device__ inline void uniform_tile_out(uint32_t *sc /* >= kMT + 1 words */, uint32_t *s_red, uint64_t *mbw,
                                         uint64_t *cw, uint64_t *pfx, uint32_t *ti, uint32_t t0, uint32_t t1,
                                         uint32_t blen) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t tid = FCX_TID, lane = tid & 63, wv = tid >> 6;
     auto ustep = [&](uint32_t p) -> uint32_t { return m_len(m_uniform(p, blen)) + 1; };
 #if FCX_RUNS
     // (the runs unit's shards are mostly uniform tiles, zeros: the closed forms)  m_uniform is a match
@@ -862,7 +883,7 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
     __shared__ uint32_t s_chg[2];
     __shared__ uint32_t s_red[4 * kWaves];   // cross-wave scan partials (rmode_walk: exits + 3 scans)
 
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = FCX_TID;
     const uint32_t b = bx / L.tpb, k = bx % L.tpb;
     const uint64_t bstart = (uint64_t)b * L.B;
     const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
@@ -1216,6 +1237,12 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
         // K: binary search for the smallest count with at most kHotCap longer ranges
         auto nrange = [&](uint32_t u) -> uint32_t { return rng[u] == 0xFFFFFFFFu ? 0u : rng[u] >> 16; };
         uint32_t klo = 0, khi = wave_max_dpp(nmax);
+#if FCX_SHORTK
+        // a wave whose longest range is short takes every range whole in pass A: no K search, no
+        // pass B (its ballots, scans, slots and read-back cost more than the few extra pass-A steps)
+        const uint32_t wmax = khi;
+        if (wmax <= FCX_SHORTK) klo = khi;
+#endif
         while (klo < khi) {
             const uint32_t mid = (klo + khi) >> 1;
             uint32_t c = 0;
@@ -1274,6 +1301,9 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
             }
         }
         // pass B: the hot queries' entries from K on, flattened over the wave
+#if FCX_SHORTK
+        if (K < wmax) {
+#endif
         bool hot[kIlp];
         uint32_t slot[kIlp], hbase[kIlp], T = 0, nh = 0;
 #pragma unroll
@@ -1363,6 +1393,9 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
                 if (b >> 31) rng[u] = 0xFFFFFFFFu;
                 else best[u] = b;
             }
+#if FCX_SHORTK
+        }
+#endif
 #pragma unroll
         for (uint32_t u = 0; u < kIlp; u++) {
             const uint32_t x = xpk[u] & 0x1FFFu;
@@ -1611,10 +1644,13 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
                                               uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg_in,
                                               MatchRoute rt) {
     uint32_t bx = xcd_tile(blockIdx.x, gridDim.x);
-    if (rt.list) {   // (both loads in flight together: the grid never exceeds the list's storage)
+    if (rt.list) {
+        // both loads in flight together (the grid never exceeds the list's storage, so list[bx] is
+        // always readable); the empty asm keeps the compiler from sinking the second below the test
         const uint32_t c = *rt.cnt, t = rt.list[bx];
+        asm volatile("" ::"v"(c), "v"(t));
         if (bx >= c) return;
-        bx = t;
+        bx = uni(t);
     }
     match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rt);
 }
@@ -1625,7 +1661,7 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
 // grid the host gave that unit (rest.grid[u]; a unit not launched has grid 0), i.e. the tiles of
 // kinds the host did not expect.  A fixed grid of workgroups loops over them (the count is only
 // known on the device); with none left every workgroup exits at once.
-__global__ __launch_bounds__(kMT, 8) void k_match_rest(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
+__global__ __launch_bounds__(kMT, FCX_REST_WAVES) void k_match_rest(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                                    uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                                    uint64_t *__restrict__ chain_pfx, uint32_t *__restrict__ tinfo,
                                                    uint32_t *__restrict__ mtok, RouteRest rest) {
