@@ -305,6 +305,9 @@ void fcx_loop_destroy(fcx_loop *hub);
 int fcx_dist_init_loop(fcx_dist **d, fcx_loop *hub, int rank);
 /* every rank of an nranks job in one handle on one device (the fcx_dist_init_local form) */
 int fcx_dist_init_loop_local(fcx_dist **d, int nranks, int device, uint32_t timeout_ms);
+/* Rank 0 of the last fcx_dist_compress_gather: device ms of its final moves of the peers' bytes
+ * behind its own segment (N - 1 copies, hipEvents on its stream); -1 on a peer or before any. */
+int fcx_dist_gather_copy_ms(fcx_dist *d, float *ms);
 /* Testing: a peer of fcx_dist_compress_gather treats sub-batch `piece` as failed after the
  * earlier pieces are queued (as device error bits would); -1 = off. */
 int fcx_dist_debug_fail(fcx_dist *d, int piece);

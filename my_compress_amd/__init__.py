@@ -134,6 +134,8 @@ def lib():
     L.fcx_dist_init_loop_local.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int,
                                            ctypes.c_uint32]
     L.fcx_dist_debug_fail.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if hasattr(L, "fcx_dist_gather_copy_ms"):
+        L.fcx_dist_gather_copy_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
     L.fcx_last_error.restype = ctypes.c_char_p
     L.fcx_version.restype = ctypes.c_char_p
     _lib = L
@@ -540,6 +542,13 @@ class Dist:
     def debug_fail(self, piece: int):
         """testing: as a peer of compress_gather, treat sub-batch `piece` as failed (-1 = off)"""
         _check(lib().fcx_dist_debug_fail(self._h, piece), "fcx_dist_debug_fail")
+
+    def gather_copy_ms(self) -> float:
+        """rank 0 of the last compress_gather: device ms of its final moves of the peers' bytes
+        behind its own segment (-1 on a peer)"""
+        v = ctypes.c_float(-1.0)
+        _check(lib().fcx_dist_gather_copy_ms(self._h, ctypes.byref(v)), "fcx_dist_gather_copy_ms")
+        return float(v.value)
 
     def close(self):
         if self._h:

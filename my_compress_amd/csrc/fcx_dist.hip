@@ -422,6 +422,8 @@ struct fcx_dist {
     uint64_t stage_cap = 0;
     uint8_t *d_drain = nullptr;      // rank 0: a piece beyond its peer's bound, received and dropped
     uint64_t drain_cap = 0;
+    hipEvent_t copy_ev[2] = {nullptr, nullptr};   // rank 0: around the final moves of the peers' bytes
+    float copy_ms = -1.f;            // their duration in the last gather (-1: none timed)
     int fail_piece = -1;             // testing: a peer treats this piece as failed (fcx_dist_debug_fail)
 };
 
@@ -502,6 +504,7 @@ int ensure_gather(fcx_dist *d, uint64_t stage) {
         DHIP(hipMemcpy(d->d_ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice));
         d->ev.assign(FCX_DIST_MAX_SUB, nullptr);
         for (auto &e : d->ev) DHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto &e : d->copy_ev) DHIP(hipEventCreate(&e));
     }
     if (stage > d->stage_cap) {
         if (d->d_stage) DHIP(hipFree(d->d_stage));
@@ -521,6 +524,10 @@ void release_gather(fcx_dist *d) {
     for (auto e : d->ev)
         if (e) (void)hipEventDestroy(e);
     d->ev.clear();
+    for (auto &e : d->copy_ev) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
     if (d->cst) (void)hipStreamDestroy(d->cst);
     if (d->d_words) (void)hipFree(d->d_words);
     if (d->h_words) (void)hipHostFree(d->h_words);
@@ -714,12 +721,15 @@ int gather_root(fcx_dist *d, fcx_ctx *c, const uint8_t *d_in, uint64_t n, const 
         return dfail(verdict, msg);
     }
     off = own;
+    DHIP(hipEventRecord(d->copy_ev[0], st));
     for (int r = 1; r < N; r++) {   // the peers' bytes behind the own segment, in rank order
         if (fill[r]) DHIP(hipMemcpyAsync(d_out + off, d->d_stage + soff[r], fill[r], hipMemcpyDeviceToDevice, st));
         off += fill[r];
     }
+    DHIP(hipEventRecord(d->copy_ev[1], st));
     DHIP(hipStreamSynchronize(d->cst));
     DHIP(hipStreamSynchronize(st));
+    if (hipEventElapsedTime(&d->copy_ms, d->copy_ev[0], d->copy_ev[1]) != hipSuccess) d->copy_ms = -1.f;
     *total = off;
     return FCX_OK;
 }
@@ -967,6 +977,12 @@ int fcx_dist_init_loop_local(fcx_dist **out, int nranks, int device, uint32_t ti
 }
 
 const char *fcx_dist_transport(fcx_dist *d) { return d && !d->tr.empty() ? d->tr[0]->name() : ""; }
+
+int fcx_dist_gather_copy_ms(fcx_dist *d, float *ms) {
+    if (!d || !ms) return dfail(FCX_ERR_ARG, "fcx_dist_gather_copy_ms: NULL argument");
+    *ms = d->copy_ms;
+    return FCX_OK;
+}
 
 int fcx_dist_debug_fail(fcx_dist *d, int piece) {
     if (!d) return dfail(FCX_ERR_ARG, "NULL dist");

@@ -1637,14 +1637,14 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
 // unit's list and workgroup i takes list entry i, if there is one (the entries past the grid go to
 // k_match_rest).  Either way each XCD takes a contiguous run of entries (xcd_tile).
 #if !FCX_REST
-template <bool kDev>
+template <bool kDev, bool kListed>
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
                                               uint32_t *__restrict__ tinfo, uint32_t *__restrict__ mtok, uint32_t dbg_in,
                                               MatchRoute rt) {
     uint32_t bx = xcd_tile(blockIdx.x, gridDim.x);
-    if (rt.list) {
+    if constexpr (kListed) {   // (its own instance: the list read moves the unlisted kernel's code)
         // both loads in flight together (the grid never exceeds the list's storage, so list[bx] is
         // always readable); the empty asm keeps the compiler from sinking the second below the test
         const uint32_t c = *rt.cnt, t = rt.list[bx];
@@ -1702,12 +1702,15 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
     const MatchRoute rt = route ? *route : MatchRoute{};
     const uint32_t grid = rt.list ? grid_override : L.nblocks * L.tpb;
     if (grid == 0) return;
-    if (dbg == 0)
-        hipLaunchKernelGGL(k_match<false>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u,
-                           rt);
+    if (rt.list)
+        hipLaunchKernelGGL((k_match<false, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
+                           mtok, 0u, rt);
+    else if (dbg == 0)
+        hipLaunchKernelGGL((k_match<false, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
+                           mtok, 0u, rt);
     else
-        hipLaunchKernelGGL(k_match<true>, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg,
-                           rt);
+        hipLaunchKernelGGL((k_match<true, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
+                           mtok, dbg, rt);
 }
 #endif
 

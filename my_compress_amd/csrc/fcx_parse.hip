@@ -816,8 +816,11 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     }
     const uint8_t *d = in + bstart;
     const bool al = (((uintptr_t)d) & 15) == 0;
-    uint32_t in4[4];
-    if (al && s + 16 <= blen) {
+    // (the loads above are waited for by the check: a uniform tile -- zeros -- skips the input loads,
+    // its one byte value is read below; 1 GiB of zeros no longer re-reads its GiB here)
+    uint32_t in4[4] = {0u, 0u, 0u, 0u};
+    if (uni) {
+    } else if (al && s + 16 <= blen) {
         const uint4 v4 = *(const uint4 *)(d + s);
         in4[0] = v4.x; in4[1] = v4.y; in4[2] = v4.z; in4[3] = v4.w;
     } else {
@@ -840,7 +843,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     }
     uint32_t la = 0;   // look-ahead dword (match chars past the tile end)
     const uint32_t xa = t0 + kTile + 4 * tid;
-    if (tid < kInW - kTile / 4 && xa < blen) {
+    if (!uni && tid < kInW - kTile / 4 && xa < blen) {
         if (al && xa + 4 <= blen) la = *(const uint32_t *)(d + xa);
         else
             for (uint32_t j = 0; j < 4 && xa + j < blen; j++) la |= (uint32_t)d[xa + j] << (8 * j);
@@ -854,7 +857,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
             bits = (uint32_t)(cwv >> (16 * (tid & 3))) & 0xFFFFu;
             if (t1 - s < 16) bits &= (1u << (t1 - s)) - 1u;
         }
-        const uint8_t ub = (uint8_t)in4[0];   // (lanes with tokens lie inside the tile)
+        const uint8_t ub = d[t0];   // the tile's byte value
         uint32_t v[3] = {(uint32_t)__builtin_popcount(bits), 0, 0}, tot[3];
         for (uint32_t bb = bits; bb; bb &= bb - 1) {
             const uint32_t Lm = m_len(m_uniform(s + __builtin_ctz(bb), blen));

@@ -177,6 +177,11 @@ def test_loop_hl_rand_n8_digest(cuda):
         h.update(memoryview(outs[0][:res[0]].cpu().numpy()))
         assert res[0] + 10 == want_bytes
         assert h.hexdigest() == want_sha
+        # rank 0's final moves of the 7 peers' bytes behind its segment (timed on its stream)
+        copy_ms = job.dists[0].gather_copy_ms()
+        print(f"N=8 loopback: rank-0 share {share0 / 1e4:.1f} %, final copies {copy_ms:.3f} ms", flush=True)
+        assert 0 <= copy_ms < 50, copy_ms
+        assert all(job.dists[r].gather_copy_ms() < 0 for r in range(1, N))
     finally:
         for c in ctxs:
             c.close()
