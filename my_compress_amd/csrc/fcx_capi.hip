@@ -25,11 +25,19 @@ FCX_MATCH_LAUNCHER(launch_match_nf)
 FCX_MATCH_LAUNCHER(launch_match_runs)
 FCX_MATCH_LAUNCHER(launch_match_sparse)
 #undef FCX_MATCH_LAUNCHER
-void launch_match_rest(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                       uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, const RouteRest &rest, uint32_t grid,
-                       hipStream_t st);
+// the units' looped remainders (fcx_match_rest_<unit>.hip)
+#define FCX_REST_LAUNCHER(name)                                                                               \
+    void name(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,              \
+              uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, const RouteRest &rest, const MatchRoute &rt, \
+              uint32_t grid, hipStream_t st);
+FCX_REST_LAUNCHER(launch_match_rest_sparse)
+FCX_REST_LAUNCHER(launch_match_rest_runs)
+FCX_REST_LAUNCHER(launch_match_rest_k4)
+FCX_REST_LAUNCHER(launch_match_rest_nf)
+#undef FCX_REST_LAUNCHER
 void launch_classify(const uint8_t *in, const Layout &L, uint32_t *lists, uint32_t stride, uint32_t *cnt,
                      uint8_t *tkind, hipStream_t st);
+void launch_route_mark(uint32_t *dst, const uint32_t *src, hipStream_t st);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -107,7 +115,9 @@ using MatchLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64
 constexpr int kRouteKernel[kRoutes] = {kMatchSparse, kMatchRuns, kMatchKey4, kMatchNoFilter};
 constexpr uint32_t kRouteWords = 8;         // device counters per block group (k_classify: cnt[0..5])
 constexpr uint32_t kRouteMinTiles = 8;      // a unit expected to get fewer tiles is not launched (k_match_rest)
-constexpr uint32_t kRestGrid = 512;         // k_match_rest's workgroups (2 per CU: 128 VGPRs)
+constexpr uint32_t kRestGrid = 512;         // k_match_rest_<unit>'s workgroups (2 per CU: <= 128 VGPRs)
+constexpr uint32_t kRestDirect = ~0u;       // last_grid: a direct launch (its list's remainder starts at the cover)
+constexpr uint32_t kCoverWord = 6;          // route counter: the no-filter entries a direct launch covered
 constexpr uint64_t kRouteBytes = 4ull * kRouteWords * 8;   // route counters of kMaxGroups (= 8) groups
 constexpr uint64_t kWordBytes = 64 + kRouteBytes;          // dev_words
 static MatchLaunch match_launcher(int k) {
@@ -464,37 +474,55 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                 const uint64_t v = std::max<uint64_t>(c->hint_valid, 1);
                 for (uint32_t u = 0; u < kRoutes; u++) est[u] = (c->hint_cnt[u] * ntg + v - 1) / v;
             }
-            RouteRest rest{lists, rc, stride, {0, 0, 0, 0}};
             // the unit expected to take most of the tiles (at least half) runs over every tile of the
             // group and skips the others by their kind byte: no list read before its staging loads
             uint32_t best = 0;
             for (uint32_t u = 1; u < kRoutes; u++)
                 if (est[u] > est[best]) best = u;
             const bool direct = 2 * est[best] >= ntg;
+            MatchRoute rts[kRoutes];
+            RouteRest rest[kRoutes];
             for (uint32_t u = 0; u < kRoutes; u++) {
                 // a small margin over the estimate (its excess workgroups exit at once); the no-filter
                 // list also takes the tiles the sparse / runs units hand on
                 const uint64_t gr = est[u] >= kRouteMinTiles ? est[u] + est[u] / 16 + 32 : 0;
-                MatchRoute rt;
+                MatchRoute &rt = rts[u];
                 rt.kind = c->tkind + t0;
                 rt.mine = u;
+                rt.cnt = rc + u;
+                rest[u] = RouteRest{lists + (uint64_t)u * stride, rc + u, 0u, nullptr};
+                uint32_t grid = 0;
                 if (direct && u == best) {
-                    rest.grid[u] = ~0u;   // (every entry of its list: the direct grid has them all)
+                    // the direct grid has every entry of its list (its kind bytes); the no-filter list can
+                    // grow after it by the remainders' hand-ons: its count at the launch is recorded
+                    rest[u].start = ~0u;
+                    if (u == kRouteNoFilter) {
+                        launch_route_mark(rc + kCoverWord, rc + kRouteNoFilter, sg);
+                        rest[u].start_dev = rc + kCoverWord;
+                    }
                 } else {
-                    rest.grid[u] = (uint32_t)std::min<uint64_t>(gr, ntg);
+                    grid = (uint32_t)std::min<uint64_t>(gr, ntg);
+                    rest[u].start = grid;
                     rt.list = lists + (uint64_t)u * stride;
-                    rt.cnt = rc + u;
                 }
                 if (u == kRouteSparse || u == kRouteRuns) {
                     rt.defer_list = lists + (uint64_t)kRouteNoFilter * stride;
                     rt.defer_cnt = rc + kRouteNoFilter;
                 }
-                match_launcher(kRouteKernel[u])(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, sg, 0u, &rt,
-                                                rest.grid[u]);
-                c->last_grid[g][u] = rest.grid[u];
+                match_launcher(kRouteKernel[u])(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, sg, 0u, &rt, grid);
+                c->last_grid[g][u] = direct && u == best ? kRestDirect : grid;
             }
             if (g == 0) c->last_kernel = est[best] ? kRouteKernel[best] : kMatchGeneral;
-            launch_match_rest(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, rest, kRestGrid, sg);
+            // each unit's remainder (the no-filter one last: it takes the others' hand-ons); a direct
+            // sparse / runs / 4-byte launch leaves none
+            using RestLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64_t *, uint64_t *, uint64_t *,
+                                        uint32_t *, uint32_t *, const RouteRest &, const MatchRoute &, uint32_t,
+                                        hipStream_t);
+            const RestLaunch rest_launch[kRoutes] = {launch_match_rest_sparse, launch_match_rest_runs,
+                                                     launch_match_rest_k4, launch_match_rest_nf};
+            for (uint32_t u = 0; u < kRoutes; u++)
+                if (rest[u].start != ~0u || rest[u].start_dev)
+                    rest_launch[u](gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, rest[u], rts[u], kRestGrid, sg);
         }
         if (ev) HIP_TRY(hipEventRecord(ev[2], sg));
         launch_parse(gin, Lg, c->m + b0 * c->B, c->mbits + b0 * L.wpb, c->chain + b0 * L.wpb,
@@ -592,7 +620,10 @@ int fcx_ctx_route_stats(fcx_ctx *c, uint64_t *out, int n) {
             const uint32_t *r = rc + kRouteWords * g;
             for (uint32_t u = 0; u < kRoutes; u++) {
                 v[u] += r[u];
-                v[6] += r[u] > c->last_grid[g][u] ? r[u] - c->last_grid[g][u] : 0u;
+                const uint32_t s0 = c->last_grid[g][u] != kRestDirect ? c->last_grid[g][u]
+                                    : u == kRouteNoFilter                ? r[kCoverWord]
+                                                                         : r[u];
+                v[6] += r[u] > s0 ? r[u] - s0 : 0u;
             }
             v[4] += r[kRouteNoFilter] - r[4];
             v[5] += r[5];

@@ -96,11 +96,11 @@ struct MatchRoute {
     uint8_t *kind = nullptr;          // per tile: its unit (k_classify; a hand-on rewrites it).  With no
     uint32_t mine = 0;                //   list, the grid covers every tile and searches those of kind mine
 };
-struct RouteRest {                    // k_match_rest: list entries past the grid each unit was given
-    const uint32_t *lists;            // kRoutes lists of list_stride entries
-    const uint32_t *cnt;              // kRoutes counts
-    uint32_t list_stride;
-    uint32_t grid[kRoutes];           // grid of unit u's launch (0: not launched)
+struct RouteRest {                    // k_match_rest_<unit>: its list's entries no unit launch covered
+    const uint32_t *list;
+    const uint32_t *cnt;
+    uint32_t start;                   // the first of them: the launch's grid (0: not launched) ...
+    const uint32_t *start_dev;        // ... or, when set, read here (a direct launch's cover)
 };
 
 // ---- wave64 helpers --------------------------------------------------------

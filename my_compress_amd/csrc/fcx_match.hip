@@ -88,9 +88,9 @@
 #ifndef FCX_SHORTK
 #define FCX_SHORTK 0
 #endif
-// FCX_REST (fcx_match_rest.hip): the general kernel's tile body in k_match_rest, the loop over the
-// tiles a routed call's unit launches did not cover (fcx_route.hip).  Its own translation unit, so
-// the general k_match keeps its code generation.
+// FCX_REST (fcx_match_rest_<unit>.hip): the unit's tile body in k_match_rest_<unit>, a loop over the
+// entries of the unit's list that its launch did not cover (fcx_route.hip).  Its own translation
+// unit, so the unit's k_match keeps its code generation.
 #ifndef FCX_REST
 #define FCX_REST 0
 #endif
@@ -112,15 +112,23 @@
 #if FCX_KEY4
 #define k_match k_match_k4
 #define launch_match launch_match_k4
+#define k_match_rest k_match_rest_k4
+#define launch_match_rest launch_match_rest_k4
 #elif FCX_NOFILTER
 #define k_match k_match_nf
 #define launch_match launch_match_nf
+#define k_match_rest k_match_rest_nf
+#define launch_match_rest launch_match_rest_nf
 #elif FCX_SPARSE
 #define k_match k_match_sparse
 #define launch_match launch_match_sparse
+#define k_match_rest k_match_rest_sparse
+#define launch_match_rest launch_match_rest_sparse
 #elif FCX_RUNS
 #define k_match k_match_runs
 #define launch_match launch_match_runs
+#define k_match_rest k_match_rest_runs
+#define launch_match_rest launch_match_rest_runs
 #endif
 #if FCX_RUNS
 #define FCX_RMODE_CALL __forceinline__
@@ -1083,6 +1091,9 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
         // not sparse, in a routed call: the tile goes on to the no-filter unit's list (launched after
         // this one), which searches it by buckets.  Nothing of it has been written yet.  (The run
         // table below overflows on match-dense tiles and leaves them to the stitch's serial walk.)
+        // Not in the direct kernel (k_match<kDev, false> passes a null list: the branch is compiled
+        // out there, where it cost the sparse unit ~4 % on random data): a misfiled tile in the unit
+        // that has most of the call's tiles takes the run table below.
         if (tid == 0) {
             rt.defer_list[atomicAdd(rt.defer_cnt, 1u)] = bx;
             rt.kind[bx] = (uint8_t)kRouteNoFilter;   // (a direct no-filter launch finds it by its kind)
@@ -1652,40 +1663,40 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         if (bx >= c) return;
         bx = uni(t);
     }
-    match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rt);
+    if constexpr (kListed) {
+        match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rt);
+    } else {
+        MatchRoute rd = rt;
+        rd.defer_list = nullptr;   // (a constant: the hand-on branch folds away)
+        match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rd);
+    }
 }
 #endif
 
 #if FCX_REST
-// The routed call's remainder, by the general kernel: the entries of each unit's list past the
-// grid the host gave that unit (rest.grid[u]; a unit not launched has grid 0), i.e. the tiles of
-// kinds the host did not expect.  A fixed grid of workgroups loops over them (the count is only
-// known on the device); with none left every workgroup exits at once.
+// The routed call's remainder for this unit: the entries of its list from rest.start on (past its
+// launch's grid; every entry when it was not launched; past a direct launch's cover) -- tiles of a
+// kind the host's estimate did not foresee, and the no-filter list's late hand-ons.  A fixed grid of
+// workgroups loops over them (the count is only known on the device); with none left every
+// workgroup exits at once.  Looped, the body needs up to 128 VGPRs, so FCX_REST_WAVES is 4.
 __global__ __launch_bounds__(kMT, FCX_REST_WAVES) void k_match_rest(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                                    uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                                    uint64_t *__restrict__ chain_pfx, uint32_t *__restrict__ tinfo,
-                                                   uint32_t *__restrict__ mtok, RouteRest rest) {
-    uint32_t left[kRoutes], total = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < kRoutes; u++) {
-        const uint32_t c = rest.cnt[u];
-        left[u] = c > rest.grid[u] ? c - rest.grid[u] : 0u;
-        total += left[u];
-    }
-    const MatchRoute none{};
-    for (uint32_t i = blockIdx.x; i < total; i += gridDim.x) {
-        uint32_t u = 0, p = i;
-        while (u + 1 < kRoutes && p >= left[u]) { p -= left[u]; u++; }
-        const uint32_t bx = rest.lists[(uint64_t)u * rest.list_stride + rest.grid[u] + p];
-        match_tile<false>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u, bx, none);
+                                                   uint32_t *__restrict__ mtok, RouteRest rest, MatchRoute rt) {
+    const uint32_t c = *rest.cnt, s0 = rest.start_dev ? *rest.start_dev : rest.start;
+    rt.list = nullptr;   // (the tiles come from the loop; kind bytes and hand-ons as in the routed launch)
+    for (uint32_t p = s0 + blockIdx.x; p < c; p += gridDim.x) {
+        const uint32_t bx = rest.list[p];
+        match_tile<false>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u, bx, rt);
         __syncthreads();   // the next tile's staging overwrites the LDS this one read
     }
 }
 
 void launch_match_rest(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
-                       uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, const RouteRest &rest, uint32_t grid,
-                       hipStream_t st) {
-    hipLaunchKernelGGL(k_match_rest, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, rest);
+                       uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, const RouteRest &rest, const MatchRoute &rt,
+                       uint32_t grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_match_rest, dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo, mtok, rest,
+                       rt);
 }
 #endif
 

@@ -162,6 +162,17 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
     }
 }
 
+// a direct no-filter launch covers its list up to the count at its start (its kind bytes include the
+// sparse / runs units' hand-ons until then): recorded on the stream just before it, so its remainder
+// takes only the later hand-ons
+__global__ void k_route_mark(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src) {
+    if (threadIdx.x == 0) *dst = *src;
+}
+
+void launch_route_mark(uint32_t *dst, const uint32_t *src, hipStream_t st) {
+    hipLaunchKernelGGL(k_route_mark, dim3(1), dim3(64), 0, st, dst, src);
+}
+
 void launch_classify(const uint8_t *in, const Layout &L, uint32_t *lists, uint32_t stride, uint32_t *cnt,
                      uint8_t *tkind, hipStream_t st) {
     const uint32_t nt = L.nblocks * L.tpb;
