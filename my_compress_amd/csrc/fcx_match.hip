@@ -112,24 +112,34 @@
 #if FCX_KEY4
 #define k_match k_match_k4
 #define launch_match launch_match_k4
+#define launch_match_listed launch_match_k4_listed
 #define k_match_rest k_match_rest_k4
 #define launch_match_rest launch_match_rest_k4
 #elif FCX_NOFILTER
 #define k_match k_match_nf
 #define launch_match launch_match_nf
+#define launch_match_listed launch_match_nf_listed
 #define k_match_rest k_match_rest_nf
 #define launch_match_rest launch_match_rest_nf
 #elif FCX_SPARSE
 #define k_match k_match_sparse
 #define launch_match launch_match_sparse
+#define launch_match_listed launch_match_sparse_listed
 #define k_match_rest k_match_rest_sparse
 #define launch_match_rest launch_match_rest_sparse
 #elif FCX_RUNS
 #define k_match k_match_runs
 #define launch_match launch_match_runs
+#define launch_match_listed launch_match_runs_listed
 #define k_match_rest k_match_rest_runs
 #define launch_match_rest launch_match_rest_runs
 #endif
+// FCX_LISTED (fcx_match_<unit>_listed.hip): the unit's listed kernel instance alone (routed calls,
+// fcx_route.hip), in its own translation unit: next to it the direct instance's code moved
+#ifndef FCX_LISTED
+#define FCX_LISTED 0
+#endif
+#define FCX_UNIT (FCX_KEY4 || FCX_NOFILTER || FCX_SPARSE || FCX_RUNS)
 #if FCX_RUNS
 #define FCX_RMODE_CALL __forceinline__
 #else
@@ -1700,7 +1710,19 @@ void launch_match_rest(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t
 }
 #endif
 
-#if !FCX_REST
+#if FCX_LISTED
+void launch_match_listed(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                         uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, const MatchRoute &rt,
+                         uint32_t grid) {
+    hipLaunchKernelGGL((k_match<false, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
+                       mtok, 0u, rt);
+}
+#elif !FCX_REST
+#if FCX_UNIT
+void launch_match_listed(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                         uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, const MatchRoute &rt,
+                         uint32_t grid);   // (fcx_match_<unit>_listed.hip)
+#endif
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                   uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override, const MatchRoute *route,
                   uint32_t grid_override) {
@@ -1713,10 +1735,11 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
     const MatchRoute rt = route ? *route : MatchRoute{};
     const uint32_t grid = rt.list ? grid_override : L.nblocks * L.tpb;
     if (grid == 0) return;
-    if (rt.list)
-        hipLaunchKernelGGL((k_match<false, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
-                           mtok, 0u, rt);
-    else if (dbg == 0)
+    if (rt.list) {
+#if FCX_UNIT
+        launch_match_listed(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, st, rt, grid);
+#endif
+    } else if (dbg == 0)
         hipLaunchKernelGGL((k_match<false, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
                            mtok, 0u, rt);
     else

@@ -1,0 +1,7 @@
+// fcx_match_nf_listed.hip — the nf unit's listed kernel instance (k_match<false, true>: its tiles from
+// the unit's list in a routed call, fcx_route.hip).  Its own translation unit: beside the direct
+// instance it moved that kernel's code (fcx_match.hip FCX_LISTED).
+#define FCX_NOFILTER 1
+#define FCX_UNIT_ILP 2
+#define FCX_LISTED 1
+#include "fcx_match.hip"

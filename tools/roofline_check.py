@@ -14,12 +14,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r04"
 line = json.loads(open(os.path.join(ROOT, "profiles", f"{tag}_bench_n1.json")).read().strip().splitlines()[-1])
 legs = {"rand": line}
-legs.update({k: line[k] for k in ("c2", "text", "c3", "zeros", "runs", "dna") if isinstance(line.get(k), dict)})
+legs.update({k: line[k] for k in ("c2", "text", "c3", "zeros", "runs", "dna", "mix") if isinstance(line.get(k), dict)})
 print(f"{'leg':6s} {'kernel':10s} {'bench kernel ms':>15s} {'rocprof avg ms':>15s} {'bench frac':>11s} {'rocprof frac':>13s}")
 for leg, v in legs.items():
     r = v["roofline"]
     path = os.path.join(ROOT, "profiles", f"{tag}_kernel_stats_{leg}.csv")
     avg = None
+    if not os.path.exists(path):
+        continue
     for row in csv.DictReader(open(path)):
         if row["Name"].split("(")[0].replace("void ", "").replace("fcx::", "").split("<")[0] == r["kernel"]:
             avg = float(row["AverageNs"]) / 1e6
