@@ -487,9 +487,36 @@ def transition_leg(dev, block=1 << 20, shard_mib=256, calls=4):
     finally:
         ctx.close()
     steady = min(ms["text"][1:])
+    # the stream path (host memory in and out, fcx_compress_host in 64 MiB shards) over rand then
+    # text on one context, against the two parts streamed apart on fresh contexts
+    import ctypes
+
+    hosts = {k: make_input(k, SEEDS[k], 0, n) for k in ("rand", "text")}
+    both = torch.cat([hosts["rand"], hosts["text"]]).pin_memory()
+    out = ctypes.create_string_buffer(mc.shard_bound(2 * n, block))
+    got = ctypes.c_uint64(0)
+
+    def stream(buf, nb):
+        c = mc.Context(dev.index, block, 64 << 20)
+        try:
+            t0 = time.perf_counter()
+            mc._check(mc.lib().fcx_compress_host(c._h, ctypes.cast(buf.data_ptr(), ctypes.POINTER(ctypes.c_uint8)), nb,
+                                                 ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), len(out),
+                                                 ctypes.byref(got)), "fcx_compress_host")
+            return (time.perf_counter() - t0) * 1e3
+        finally:
+            c.close()
+
+    t_rand = min(stream(hosts["rand"], n) for _ in range(2))
+    t_text = min(stream(hosts["text"], n) for _ in range(2))
+    t_both = min(stream(both, 2 * n) for _ in range(2))
     return {"shard_mib": shard_mib, "rand_ms": ms["rand"], "text_ms": ms["text"], "rest_tiles": rest,
             "first_text_vs_steady": ms["text"][0] / steady,
-            "note": "synchronous calls on one context: rand x %d then text x %d" % (calls, calls)}
+            "stream_ms": {"rand": t_rand, "text": t_text, "rand_then_text": t_both},
+            "stream_vs_parts": t_both / (t_rand + t_text),
+            "note": "synchronous calls on one context: rand x %d then text x %d; stream: fcx_compress_host in "
+                    "64 MiB shards (PCIe both ways), rand then text on one fresh context against each part "
+                    "on its own" % (calls, calls)}
 
 
 def host_leg(host, n, block, reps=3):
@@ -919,7 +946,8 @@ def main():
         if "weak" in line:
             brief("weak", line["weak"])
         if "transition" in line:
-            summ["transition"] = {"first_text_vs_steady": round(line["transition"]["first_text_vs_steady"], 3)}
+            summ["transition"] = {"first_text_vs_steady": round(line["transition"]["first_text_vs_steady"], 3),
+                                  "stream_vs_parts": round(line["transition"]["stream_vs_parts"], 3)}
         line["legs"] = summ
         print(json.dumps(line), flush=True)
     if dist:

@@ -117,7 +117,7 @@ constexpr uint32_t kRouteWords = 8;         // device counters per block group (
 constexpr uint32_t kRouteMinTiles = 8;      // a unit expected to get fewer tiles is not launched (k_match_rest)
 constexpr uint32_t kRestGrid = 512;         // k_match_rest_<unit>'s workgroups (2 per CU: <= 128 VGPRs)
 constexpr uint32_t kRestDirect = ~0u;       // last_grid: a direct launch (its list's remainder starts at the cover)
-constexpr uint32_t kCoverWord = 6;          // route counter: the no-filter entries a direct launch covered
+constexpr uint32_t kCoverWord = 6;          // route counter: the no-filter list's count at its listed launch
 constexpr uint64_t kRouteBytes = 4ull * kRouteWords * 8;   // route counters of kMaxGroups (= 8) groups
 constexpr uint64_t kWordBytes = 64 + kRouteBytes;          // dev_words
 static MatchLaunch match_launcher(int k) {
@@ -150,8 +150,8 @@ struct fcx_ctx {
     uint32_t *ctab = nullptr;          // code table
     uint8_t *ltab = nullptr, *hhdr = nullptr;
     uint64_t *blk_off = nullptr;
-    uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits; from byte 64: the route
-                                       // counters, kRouteWords u32 per block group (k_classify, the units)
+    uint64_t *dev_words = nullptr;     // [0] = total output bytes, [1] = error bits, [2] = lazy tiles (k_tree);
+                                       // from byte 64: the route counters, kRouteWords u32 per block group
     uint64_t *host_words = nullptr;    // pinned: [0..1] length reads; from byte 64 the route counters of a
                                        // recent call (copied back asynchronously after every routed call);
                                        // from byte 64 + kRouteBytes the first call's counts (waited for)
@@ -161,6 +161,7 @@ struct fcx_ctx {
     bool have_hint = false;            // a routed call has run: the estimates below are set
     uint64_t hint_cnt[kRoutes] = {};   // tiles per list (after the hand-ons) of a recent call ...
     uint64_t hint_valid = 0;           // ... out of its tiles with bytes
+    uint64_t hint_fix = 0;             // its hand-ons plus its lazy tiles (k_tree): > 0 keeps every unit listed
     uint32_t last_grid[kMaxGroups][kRoutes] = {};   // the last call's unit grids per group
     uint32_t last_groups = 0;
     bool last_routed = false, last_cold = false;
@@ -418,14 +419,18 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
     const bool routed = c->kernel == kMatchAuto;
     if (routed && c->have_hint) {
         const uint32_t *hr = (const uint32_t *)((const uint8_t *)c->host_words + 64);
-        uint64_t cnt[kRoutes] = {}, valid = 0;
+        uint64_t cnt[kRoutes] = {}, valid = 0, fix = 0;
         for (uint32_t g = 0; g < kMaxGroups; g++) {
             for (uint32_t u = 0; u < kRoutes; u++) cnt[u] += __atomic_load_n(&hr[kRouteWords * g + u], __ATOMIC_RELAXED);
             valid += __atomic_load_n(&hr[kRouteWords * g + 5], __ATOMIC_RELAXED);
+            fix += __atomic_load_n(&hr[kRouteWords * g + kRouteNoFilter], __ATOMIC_RELAXED) -
+                   __atomic_load_n(&hr[kRouteWords * g + 4], __ATOMIC_RELAXED);
         }
+        fix += (uint32_t)__atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);   // lazy tiles (k_tree)
         if (valid) {
             for (uint32_t u = 0; u < kRoutes; u++) c->hint_cnt[u] = cnt[u];
             c->hint_valid = valid;
+            c->hint_fix = fix;
         }
     }
     c->last_routed = routed;
@@ -474,15 +479,26 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                 const uint64_t v = std::max<uint64_t>(c->hint_valid, 1);
                 for (uint32_t u = 0; u < kRoutes; u++) est[u] = (c->hint_cnt[u] * ntg + v - 1) / v;
             }
-            // the unit expected to take most of the tiles (at least half) runs over every tile of the
-            // group and skips the others by their kind byte: no list read before its staging loads
+            // the unit expected to take most of the tiles (at least half) runs first, direct over every
+            // tile of the group: it drops the others by their kind byte -- or, when the estimate gives
+            // it (nearly) all tiles, it searches every tile with the unrouted kernel's exact code, and
+            // the few tiles of other kinds are searched again by their own units afterwards (the last
+            // writer's outputs are complete).  The others run over their lists.
             uint32_t best = 0;
             for (uint32_t u = 1; u < kRoutes; u++)
                 if (est[u] > est[best]) best = u;
-            const bool direct = 2 * est[best] >= ntg;
+            // (a recent call with hand-ons or lazy tiles -- tiles its units' samples misfiled -- keeps
+            // every unit listed: only listed sparse / runs launches hand such tiles on)
+            const bool direct = 2 * est[best] >= ntg && c->hint_fix == 0;
+            const bool every = direct && 64 * est[best] >= 63ull * ntg;
+            uint32_t order[kRoutes], no = 0;
+            if (direct) order[no++] = best;
+            for (uint32_t u = 0; u < kRoutes; u++)
+                if (!(direct && u == best)) order[no++] = u;
             MatchRoute rts[kRoutes];
             RouteRest rest[kRoutes];
-            for (uint32_t u = 0; u < kRoutes; u++) {
+            for (uint32_t q = 0; q < kRoutes; q++) {
+                const uint32_t u = order[q];
                 // a small margin over the estimate (its excess workgroups exit at once); the no-filter
                 // list also takes the tiles the sparse / runs units hand on
                 const uint64_t gr = est[u] >= kRouteMinTiles ? est[u] + est[u] / 16 + 32 : 0;
@@ -492,24 +508,34 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                 rt.cnt = rc + u;
                 rest[u] = RouteRest{lists + (uint64_t)u * stride, rc + u, 0u, nullptr};
                 uint32_t grid = 0;
+                MatchRoute launch = rt;
                 if (direct && u == best) {
-                    // the direct grid has every entry of its list (its kind bytes); the no-filter list can
-                    // grow after it by the remainders' hand-ons: its count at the launch is recorded
+                    // the direct launch (first) has every entry of its list; the no-filter list grows by
+                    // later hand-ons, past the entries the classifier filed (cnt[4])
                     rest[u].start = ~0u;
-                    if (u == kRouteNoFilter) {
-                        launch_route_mark(rc + kCoverWord, rc + kRouteNoFilter, sg);
-                        rest[u].start_dev = rc + kCoverWord;
-                    }
+                    if (u == kRouteNoFilter) rest[u].start_dev = rc + 4;
+                    if (every) launch = MatchRoute{};   // (unrouted code: no kind check, no hand-on)
                 } else {
                     grid = (uint32_t)std::min<uint64_t>(gr, ntg);
                     rest[u].start = grid;
                     rt.list = lists + (uint64_t)u * stride;
+                    launch = rt;
+                    if (u == kRouteNoFilter && grid) {
+                        // covers min(grid, its count now); later hand-ons land past that count, possibly
+                        // below the grid: its remainder starts at the smaller of the two
+                        launch_route_mark(rc + kCoverWord, rc + kRouteNoFilter, sg);
+                        rest[u].start_dev = rc + kCoverWord;
+                    }
                 }
                 if (u == kRouteSparse || u == kRouteRuns) {
                     rt.defer_list = lists + (uint64_t)kRouteNoFilter * stride;
                     rt.defer_cnt = rc + kRouteNoFilter;
+                    if (launch.list || launch.kind) {
+                        launch.defer_list = rt.defer_list;
+                        launch.defer_cnt = rt.defer_cnt;
+                    }
                 }
-                match_launcher(kRouteKernel[u])(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, sg, 0u, &rt, grid);
+                match_launcher(kRouteKernel[u])(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, sg, 0u, &launch, grid);
                 c->last_grid[g][u] = direct && u == best ? kRestDirect : grid;
             }
             if (g == 0) c->last_kernel = est[best] ? kRouteKernel[best] : kMatchGeneral;
@@ -553,8 +579,8 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         for (uint32_t u = 0; u < kRoutes; u++) c->hint_cnt[u] = cold_cnt[u];
         c->hint_valid = cold_valid;
     }
-    if (routed) {   // the route counters back for the next calls' estimates (asynchronous)
-        HIP_TRY(hipMemcpyAsync((uint8_t *)c->host_words + 64, (uint8_t *)c->dev_words + 64, kRouteBytes,
+    if (routed) {   // the lazy tiles and route counters back for the next calls' estimates (asynchronous)
+        HIP_TRY(hipMemcpyAsync((uint8_t *)c->host_words + 16, (uint8_t *)c->dev_words + 16, 48 + kRouteBytes,
                                hipMemcpyDeviceToHost, st));
         c->have_hint = true;
     }
@@ -620,9 +646,11 @@ int fcx_ctx_route_stats(fcx_ctx *c, uint64_t *out, int n) {
             const uint32_t *r = rc + kRouteWords * g;
             for (uint32_t u = 0; u < kRoutes; u++) {
                 v[u] += r[u];
-                const uint32_t s0 = c->last_grid[g][u] != kRestDirect ? c->last_grid[g][u]
-                                    : u == kRouteNoFilter                ? r[kCoverWord]
-                                                                         : r[u];
+                uint32_t s0 = c->last_grid[g][u] != kRestDirect ? c->last_grid[g][u]
+                              : u == kRouteNoFilter                ? r[4]
+                                                                   : r[u];
+                if (u == kRouteNoFilter && c->last_grid[g][u] != kRestDirect && c->last_grid[g][u])
+                    s0 = std::min(s0, r[kCoverWord]);
                 v[6] += r[u] > s0 ? r[u] - s0 : 0u;
             }
             v[4] += r[kRouteNoFilter] - r[4];

@@ -99,8 +99,9 @@ struct MatchRoute {
 struct RouteRest {                    // k_match_rest_<unit>: its list's entries no unit launch covered
     const uint32_t *list;
     const uint32_t *cnt;
-    uint32_t start;                   // the first of them: the launch's grid (0: not launched) ...
-    const uint32_t *start_dev;        // ... or, when set, read here (a direct launch's cover)
+    uint32_t start;                   // the first of them: the launch's grid (0: not launched; ~0: direct) ...
+    const uint32_t *start_dev;        // ... or, when set, the smaller of it and the count read here (the
+                                      //   entries the no-filter launch covered; later ones are hand-ons)
 };
 
 // ---- wave64 helpers --------------------------------------------------------

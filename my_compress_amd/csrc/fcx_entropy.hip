@@ -138,6 +138,9 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / kStreams, s = blockIdx.x % kStreams;
     BlockInfo &bi = binfo[b];
+    // the call's lazy tiles (k_stitch walked them serially), for the routing of later calls
+    // (fcx_capi.hip: a unit that left tiles lazy is launched over its list, where hand-ons work)
+    if (s == 0 && tid == 0 && bi.lazy_tiles) atomicAdd(err + 2, bi.lazy_tiles);
     if (!stream_active(bi, s)) {
         if (tid == 0) { bi.hdrlen[s] = 0; bi.nwords[s] = 0; }
         return;

@@ -1658,7 +1658,12 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
 // unit's list and workgroup i takes list entry i, if there is one (the entries past the grid go to
 // k_match_rest).  Either way each XCD takes a contiguous run of entries (xcd_tile).
 #if !FCX_REST
-template <bool kDev, bool kListed>
+// kRouted = false: the route is a constant empty one (unrouted calls, and a direct launch over a call
+// whose tiles the estimate gives all to this unit): the list read, the kind check and the hand-on
+// branch fold away, and the kernel is the unrouted unit's code exactly.  Every unit is exact for any
+// tile, and each tile's outputs are complete from whichever kernel wrote them last, so a tile of
+// another kind searched here is searched again by its own unit (launched after this one).
+template <bool kDev, bool kListed, bool kRouted>
 __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in, Layout L, uint32_t *__restrict__ m,
                                               uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                               uint64_t *__restrict__ chain_pfx,
@@ -1675,10 +1680,13 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
     }
     if constexpr (kListed) {
         match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rt);
-    } else {
+    } else if constexpr (kRouted) {
         MatchRoute rd = rt;
         rd.defer_list = nullptr;   // (a constant: the hand-on branch folds away)
         match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rd);
+    } else {
+        const MatchRoute none{};   // (constant: list, kind check and hand-on all fold away)
+        match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, none);
     }
 }
 #endif
@@ -1693,7 +1701,7 @@ __global__ __launch_bounds__(kMT, FCX_REST_WAVES) void k_match_rest(const uint8_
                                                    uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                                    uint64_t *__restrict__ chain_pfx, uint32_t *__restrict__ tinfo,
                                                    uint32_t *__restrict__ mtok, RouteRest rest, MatchRoute rt) {
-    const uint32_t c = *rest.cnt, s0 = rest.start_dev ? *rest.start_dev : rest.start;
+    const uint32_t c = *rest.cnt, s0 = rest.start_dev ? min(rest.start, *rest.start_dev) : rest.start;
     rt.list = nullptr;   // (the tiles come from the loop; kind bytes and hand-ons as in the routed launch)
     for (uint32_t p = s0 + blockIdx.x; p < c; p += gridDim.x) {
         const uint32_t bx = rest.list[p];
@@ -1714,8 +1722,8 @@ void launch_match_rest(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t
 void launch_match_listed(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
                          uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, const MatchRoute &rt,
                          uint32_t grid) {
-    hipLaunchKernelGGL((k_match<false, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
-                       mtok, 0u, rt);
+    hipLaunchKernelGGL((k_match<false, true, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
+                       tinfo, mtok, 0u, rt);
 }
 #elif !FCX_REST
 #if FCX_UNIT
@@ -1739,12 +1747,15 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
 #if FCX_UNIT
         launch_match_listed(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, st, rt, grid);
 #endif
-    } else if (dbg == 0)
-        hipLaunchKernelGGL((k_match<false, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
-                           mtok, 0u, rt);
+    } else if (rt.kind && FCX_UNIT)   // direct, checked: tiles of other kinds end at their kind byte
+        hipLaunchKernelGGL((k_match<false, false, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
+                           tinfo, mtok, 0u, rt);
+    else if (dbg == 0)   // unrouted, or direct over every tile
+        hipLaunchKernelGGL((k_match<false, false, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
+                           tinfo, mtok, 0u, rt);
     else
-        hipLaunchKernelGGL((k_match<true, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx, tinfo,
-                           mtok, dbg, rt);
+        hipLaunchKernelGGL((k_match<true, false, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
+                           tinfo, mtok, dbg, rt);
 }
 #endif
 

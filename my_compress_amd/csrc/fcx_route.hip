@@ -162,9 +162,9 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
     }
 }
 
-// a direct no-filter launch covers its list up to the count at its start (its kind bytes include the
-// sparse / runs units' hand-ons until then): recorded on the stream just before it, so its remainder
-// takes only the later hand-ons
+// the no-filter list's count just before its listed launch: the launch covers its entries up to
+// min(grid, that count); the sparse / runs remainders hand on later tiles past it, which the
+// no-filter remainder then takes (fcx_capi.hip)
 __global__ void k_route_mark(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src) {
     if (threadIdx.x == 0) *dst = *src;
 }

@@ -59,8 +59,8 @@ def test_mixed_blocks_every_unit(cuda, block):
 
 def test_kind_changes_between_calls(cuda):
     """one context, consecutive calls of different kinds: the first tiles of a kind the estimate
-    did not foresee are searched by k_match_rest (the general kernel), and the bytes stay exact;
-    the call after sizes the new kind's unit from the new counts"""
+    did not foresee are searched by their unit's looped remainder (k_match_rest_<unit>), and the
+    bytes stay exact; the call after sizes the new kind's unit from the new counts"""
     block = 1 << 20
     ctx = mc.Context(0, block, 4 << 20)
     try:
@@ -79,25 +79,54 @@ def test_kind_changes_between_calls(cuda):
 
 def test_misfiled_tiles_handed_on(cuda):
     """tiles whose sample looks random (all 256 byte values) but which repeat within the window:
-    the classifier files them for the sparse unit, whose repeat filter refuses them; they are
-    handed on to the no-filter unit (never to the whole-tile run table) and the bytes are exact"""
-    rng = random.Random(5)
-    perm = list(range(256))
-    parts = []
-    for _ in range(64):
-        rng.shuffle(perm)
-        unit = bytes(perm)
-        parts.append(unit * 8 + inputs.generate("text", rng.randrange(1 << 20), 2048))
-    data = b"".join(parts)
+    the classifier files them for the sparse unit, whose repeat filter refuses them.  The first call
+    gives the sparse unit every tile directly (no hand-on branch there): its run table overflows and
+    the tiles go lazy -- slow, still exact; that call's lazy tiles keep the next calls' units listed,
+    where the sparse unit hands them on to the no-filter unit and no tile stays lazy"""
+    data = _misfiled(5, 64)
     block = 1 << 20
     ctx = mc.Context(0, block, len(data))
     try:
-        for call in range(2):
-            assert _compress(ctx, cuda, data, block) == oracle.compress_file(data, block)
-            rs = ctx.route_stats()
-            assert rs["handed_on"] > 0, rs
-            st = ctx.stats()
-            assert st["lazy_tiles"] == 0, st
+        want = oracle.compress_file(data, block)
+        for call in range(3):
+            assert _compress(ctx, cuda, data, block) == want, call
+            rs, st = ctx.route_stats(), ctx.stats()
+            if call > 0:
+                assert rs["handed_on"] > 0, rs
+                assert st["lazy_tiles"] == 0, st
+    finally:
+        ctx.close()
+
+
+def _misfiled(seed: int, parts: int) -> bytes:
+    """tiles half a shuffled 256-byte unit repeated (sample: every byte value, few repeats 4 back),
+    half text: filed for the sparse unit, whose repeat filter hands them on to the no-filter unit"""
+    rng = random.Random(seed)
+    perm = list(range(256))
+    out = []
+    for _ in range(parts):
+        rng.shuffle(perm)
+        out.append(bytes(perm) * 8 + inputs.generate("text", rng.randrange(1 << 20), 2048))
+    return b"".join(out)
+
+
+def test_late_hand_ons_after_listed_nofilter(cuda):
+    """a call after one whose tiles were a third each text / runs / dna (no dominant unit, so the
+    no-filter unit is launched listed with a grid sized for a third of the tiles), now on tiles the
+    sparse unit's remainder (it had no estimate) hands on: those land in the no-filter list after its
+    listed launch read the count, below its grid -- its remainder must start at the count it
+    covered, not at its grid, or those tiles are never searched"""
+    block = 1 << 20
+    prev = b"".join(inputs.generate(("text", "runs", "dna")[i % 3], 80 + i, block) for i in range(3))
+    data = _misfiled(9, 256)
+    ctx = mc.Context(0, block, len(prev))
+    try:
+        assert _compress(ctx, cuda, prev, block) == oracle.compress_file(prev, block)
+        rs = ctx.route_stats()
+        assert min(rs["nofilter"], rs["runs"], rs["key4"]) >= 240, rs   # no unit dominant
+        assert _compress(ctx, cuda, data, block) == oracle.compress_file(data, block)
+        rs = ctx.route_stats()
+        assert rs["handed_on"] > 0 and rs["rest"] > 0, rs
     finally:
         ctx.close()
 
@@ -144,3 +173,29 @@ def test_stream_across_kinds(cuda):
     assert hashlib.sha256(recs).hexdigest() == hashlib.sha256(want).hexdigest()
     small = parts[1][: 2 << 20]
     assert _compress(mc.Context(0, block, len(small)), cuda, small, block) == oracle.compress_file(small, block)
+
+
+def test_direct_every_tile_then_own_units(cuda):
+    """a shard the estimate gives (nearly) all to one unit: that unit runs first over every tile with
+    the unrouted kernel's code, and the few tiles of other kinds are searched again by their own
+    units -- the last writer's outputs must be complete.  255 random 64 KiB blocks and one text
+    block; the bytes must equal a forced unit's (every unit is exact for any tile) and the oracle's
+    on the text block, and no tile may stay lazy"""
+    block = 65536
+    rnd = inputs.generate("rand", 71, 255 * block)
+    txt = inputs.generate("text", 72, block)
+    for data in (rnd + txt, rnd[: 100 * block] + txt + rnd[100 * block:]):
+        ctx = mc.Context(0, block, len(data))
+        ref = mc.Context(0, block, len(data))
+        try:
+            ref.set_match_mode(5)   # the no-filter unit for every tile, unrouted
+            want = _compress(ref, cuda, data, block)
+            for call in range(2):
+                assert _compress(ctx, cuda, data, block) == want, call
+                rs = ctx.route_stats()
+                assert rs["sparse"] == 255 * 16 and rs["nofilter"] - rs["handed_on"] == 16, rs
+                assert ctx.stats()["lazy_tiles"] == 0
+        finally:
+            ctx.close()
+            ref.close()
+    assert _compress(mc.Context(0, block, len(txt)), cuda, txt, block) == oracle.compress_file(txt, block)
