@@ -113,24 +113,28 @@
 #define k_match k_match_k4
 #define launch_match launch_match_k4
 #define launch_match_listed launch_match_k4_listed
+#define launch_match_direct launch_match_k4_direct
 #define k_match_rest k_match_rest_k4
 #define launch_match_rest launch_match_rest_k4
 #elif FCX_NOFILTER
 #define k_match k_match_nf
 #define launch_match launch_match_nf
 #define launch_match_listed launch_match_nf_listed
+#define launch_match_direct launch_match_nf_direct
 #define k_match_rest k_match_rest_nf
 #define launch_match_rest launch_match_rest_nf
 #elif FCX_SPARSE
 #define k_match k_match_sparse
 #define launch_match launch_match_sparse
 #define launch_match_listed launch_match_sparse_listed
+#define launch_match_direct launch_match_sparse_direct
 #define k_match_rest k_match_rest_sparse
 #define launch_match_rest launch_match_rest_sparse
 #elif FCX_RUNS
 #define k_match k_match_runs
 #define launch_match launch_match_runs
 #define launch_match_listed launch_match_runs_listed
+#define launch_match_direct launch_match_runs_direct
 #define k_match_rest k_match_rest_runs
 #define launch_match_rest launch_match_rest_runs
 #endif
@@ -138,6 +142,13 @@
 // fcx_route.hip), in its own translation unit: next to it the direct instance's code moved
 #ifndef FCX_LISTED
 #define FCX_LISTED 0
+#endif
+// FCX_DIRECT (fcx_match_<unit>_direct.hip): the unit's checked direct instance alone (a routed call
+// whose estimate gives the unit most but not nearly all tiles).  Beside the unrouted instances it
+// moved their code: the helpers the kernels share are inlined differently with a third caller (the
+// runs unit went from 54 VGPRs / 12 B of stack to 62 / 40).
+#ifndef FCX_DIRECT
+#define FCX_DIRECT 0
 #endif
 #define FCX_UNIT (FCX_KEY4 || FCX_NOFILTER || FCX_SPARSE || FCX_RUNS)
 #if FCX_RUNS
@@ -869,8 +880,10 @@ __device__ inline uint32_t xcd_tile(uint32_t w, uint32_t n) {
 // One tile bx of the shard, by the whole workgroup (every return is workgroup-uniform).
 // kDev = false is the product kernel: every development / test-mode bit is compiled out.
 // k_match<true> carries them (phase exits for tools/matchphase.py through fcx_debug_match, and
-// the forced tile modes of fcx_ctx_set_match_mode, which the parity tests use).
-template <bool kDev>
+// the forced tile modes of fcx_ctx_set_match_mode, which the parity tests use).  kRt = false: the
+// unrouted code, the route's lines never emitted (a constant empty route folds them only after
+// optimisations that already moved the kernel's code generation -- 2 % on random data).
+template <bool kDev, bool kRt>
 __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const Layout L, uint32_t *__restrict__ m,
                                            uint64_t *__restrict__ mbits, uint64_t *__restrict__ chain,
                                            uint64_t *__restrict__ chain_pfx, uint32_t *__restrict__ tinfo,
@@ -963,7 +976,7 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
 #endif
     // a direct routed launch (every tile in the grid): another unit's tile ends here, its kind read
     // while the staging loads were in flight; nothing but this workgroup's LDS was written
-    if (!rt.list && rt.kind && rt.kind[bx] != rt.mine) return;
+    if (kRt && !rt.list && rt.kind && rt.kind[bx] != rt.mine) return;
     __syncthreads();
     const uint32_t npos = t1 - w0;
     const uint32_t q0 = t0 - w0;
@@ -1097,7 +1110,7 @@ __device__ __forceinline__ void match_tile(const uint8_t *__restrict__ in, const
         __syncthreads();
         if (dbg & 32u) return;
 #if FCX_NOBUCKET
-    } else if (rt.defer_list) {
+    } else if (kRt && rt.defer_list) {
         // not sparse, in a routed call: the tile goes on to the no-filter unit's list (launched after
         // this one), which searches it by buckets.  Nothing of it has been written yet.  (The run
         // table below overflows on match-dense tiles and leaves them to the stitch's serial walk.)
@@ -1679,16 +1692,17 @@ __global__ __launch_bounds__(kMT, 8) void k_match(const uint8_t *__restrict__ in
         bx = uni(t);
     }
     if constexpr (kListed) {
-        match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rt);
+        match_tile<kDev, true>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rt);
     } else if constexpr (kRouted) {
         MatchRoute rd = rt;
         rd.defer_list = nullptr;   // (a constant: the hand-on branch folds away)
-        match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rd);
+        match_tile<kDev, true>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, rd);
     } else {
         const MatchRoute none{};   // (constant: list, kind check and hand-on all fold away)
-        match_tile<kDev>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, none);
+        match_tile<kDev, false>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, dbg_in, bx, none);
     }
 }
+
 #endif
 
 #if FCX_REST
@@ -1705,7 +1719,7 @@ __global__ __launch_bounds__(kMT, FCX_REST_WAVES) void k_match_rest(const uint8_
     rt.list = nullptr;   // (the tiles come from the loop; kind bytes and hand-ons as in the routed launch)
     for (uint32_t p = s0 + blockIdx.x; p < c; p += gridDim.x) {
         const uint32_t bx = rest.list[p];
-        match_tile<false>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u, bx, rt);
+        match_tile<false, true>(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, 0u, bx, rt);
         __syncthreads();   // the next tile's staging overwrites the LDS this one read
     }
 }
@@ -1725,11 +1739,21 @@ void launch_match_listed(const uint8_t *in, const Layout &L, uint32_t *m, uint64
     hipLaunchKernelGGL((k_match<false, true, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
                        tinfo, mtok, 0u, rt);
 }
+#elif FCX_DIRECT
+void launch_match_direct(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                         uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, const MatchRoute &rt,
+                         uint32_t grid) {
+    hipLaunchKernelGGL((k_match<false, false, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
+                       tinfo, mtok, 0u, rt);
+}
 #elif !FCX_REST
 #if FCX_UNIT
 void launch_match_listed(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
                          uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, const MatchRoute &rt,
                          uint32_t grid);   // (fcx_match_<unit>_listed.hip)
+void launch_match_direct(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain,
+                         uint64_t *chain_pfx, uint32_t *tinfo, uint32_t *mtok, hipStream_t st, const MatchRoute &rt,
+                         uint32_t grid);   // (fcx_match_<unit>_direct.hip)
 #endif
 void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                   uint32_t *tinfo, uint32_t *mtok, hipStream_t st, uint32_t dbg_override, const MatchRoute *route,
@@ -1747,10 +1771,11 @@ void launch_match(const uint8_t *in, const Layout &L, uint32_t *m, uint64_t *mbi
 #if FCX_UNIT
         launch_match_listed(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, st, rt, grid);
 #endif
-    } else if (rt.kind && FCX_UNIT)   // direct, checked: tiles of other kinds end at their kind byte
-        hipLaunchKernelGGL((k_match<false, false, true>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
-                           tinfo, mtok, 0u, rt);
-    else if (dbg == 0)   // unrouted, or direct over every tile
+#if FCX_UNIT
+    } else if (rt.kind) {   // direct, checked: tiles of other kinds end at their kind byte
+        launch_match_direct(in, L, m, mbits, chain, chain_pfx, tinfo, mtok, st, rt, grid);
+#endif
+    } else if (dbg == 0)   // unrouted, or direct over every tile
         hipLaunchKernelGGL((k_match<false, false, false>), dim3(grid), dim3(kMT), 0, st, in, L, m, mbits, chain, chain_pfx,
                            tinfo, mtok, 0u, rt);
     else
