@@ -17,6 +17,7 @@ for set in "${sets[@]}"; do
   done
 done
 done
+[ -n "${NO_TRANS:-}" ] && exit 0
 timeout -k 10 300 python -u -c "
 import json, torch, bench
 print(json.dumps(bench.transition_leg(torch.device('cuda:0'))))
