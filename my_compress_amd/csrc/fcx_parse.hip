@@ -987,8 +987,8 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     uint32_t tot[3];
     const uint32_t nm_lane = v[1];
     block_scan3(v, tot, sh);
+    tot[0] = fcx::uni(tot[0]); tot[1] = fcx::uni(tot[1]); tot[2] = fcx::uni(tot[2]);
     const uint32_t tokA = tok0 + v[0], miA = mi0 + v[1];
-    uint32_t goff = g0 + v[2];
     const uint32_t fw0 = tok0 >> 5, pw0 = (uint32_t)(((uint64_t)kPBits * mi0) >> 5), gw0 = g0 >> 5;
     const uint32_t cw0 = tok0 >> 2;   // chars staged on the global dword grid
 
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         uint32_t prev = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 5; q++) {
-            const uint32_t cur = q < 4 ? in4[q] : 0u;
+            const uint32_t cur = q < 4 ? lin[4 * tid + q] : 0u;
             const uint32_t o = sb ? (cur << sb) | (prev >> (32 - sb)) : cur;
             prev = cur;
             if (q == 0 || q >= 3) { if (o) atomicOr(&lc[w0 + q], o); }
@@ -1012,13 +1012,14 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
         }
         fl = 0xFFFFu;
         nt_lane = 16;
-        hist_bytes16(in4, 16, hc);
+        const uint32_t r4[4] = {lin[4 * tid], lin[4 * tid + 1], lin[4 * tid + 2], lin[4 * tid + 3]};
+        hist_bytes16(r4, 16, hc);
     } else
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
         if ((bits >> q) & 1u) {
             const uint32_t Lm = m_len(mm[q]);
-            const uint8_t ch = Lm ? lb[s - t0 + q + Lm] : (uint8_t)(in4[q >> 2] >> (8 * (q & 3)));
+            const uint8_t ch = lb[s - t0 + q + Lm];
             lcb[tokA + nt_lane - 4 * cw0] = ch;
             atomicAdd(&hc[ch], 1u);
             if (Lm == 0) {
@@ -1026,24 +1027,44 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
             } else {
                 pacc |= (uint64_t)m_dist(mm[q]) << (kPBits * np_lane);
                 np_lane++;
-                const uint32_t qq = Lm >> 2, r = Lm & 3;
-                uint32_t pos = goff, left = qq;
-                while (left) {
-                    const uint32_t sh_ = pos & 31, n = min(left, 32 - sh_);
-                    const uint32_t msk = (n == 32 ? ~0u : ((1u << n) - 1)) << sh_;
-                    atomicOr(&lg[(pos >> 5) - gw0], msk);
-                    pos += n;
-                    left -= n;
-                }
-                pos += 1;
-                if (r) or_bits64(lg, gw0, pos, r, 2);
-                goff += qq + 3;
+                // the golomb code's offset and length go to the match's slot of lmt (free since the
+                // m values were resolved); the codes are written match-parallel below
+                lmt[miA - mi0 + np_lane - 1] = Lm;
             }
             nt_lane++;
         }
     }
     or_bits64(lf, fw0, tokA, fl, nt_lane);
     or_bits64(lp, pw0, (uint64_t)kPBits * miA, pacc, kPBits * nm_lane);
+    __syncthreads();
+    // the golomb codes (qq one-bits, a zero bit, r in 2 bits), four consecutive matches per lane, their
+    // offsets from one block scan: inside the token loop their word loop held k_emit at 78 VGPRs (6
+    // waves per SIMD; 62 and 8 waves without it).  tot[1] <= kTileMatches = 4 x 256.
+    if (tot[1]) {
+        uint32_t lm4[4], gsum = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            lm4[u] = 4 * tid + u < tot[1] ? lmt[4 * tid + u] : 0u;
+            gsum += lm4[u] ? (lm4[u] >> 2) + 3 : 0u;
+        }
+        uint32_t gtot;
+        block_scan1t(gsum, gtot, sh + 12);
+        uint32_t pos = g0 + gsum;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t Lm = lm4[u], r = Lm & 3u;
+            if (!Lm) continue;
+            uint32_t left = Lm >> 2;
+            while (left) {
+                const uint32_t sh_ = pos & 31, n = min(left, 32 - sh_);
+                atomicOr(&lg[(pos >> 5) - gw0], (n == 32 ? ~0u : ((1u << n) - 1)) << sh_);
+                pos += n;
+                left -= n;
+            }
+            if (r) or_bits64(lg, gw0, pos + 1, r, 2);
+            pos += 3;
+        }
+    }
     __syncthreads();
     if (dbg & 8u) { if (lf[tid & 63] == 0x12345u) trow[tid] = 1; return; }   // (timing: + token loop)
 
