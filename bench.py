@@ -754,10 +754,11 @@ def roofline(res, pmc_leg, pmc):
     # the match stage runs one of k_match's units (fcx_ctx_match_kernel): the kernel name is that unit's
     kernel = (res.get("match_kernel") or "k_match") if dom == "match" else f"k_{dom}" if dom else None
     rt = res.get("route") or {}
-    units = [u for u in ("sparse", "runs", "key4", "nofilter")
+    units = [u for u in ("sparse", "runs", "key4", "nofilter", "uniform")
              if rt.get(u, 0) - (rt.get("handed_on", 0) if u == "nofilter" else 0) > 0]
     if dom == "match" and len(units) > 1:   # routed over several units: the stage is their launches together
-        kernel = "k_match_{" + ",".join(dict(sparse="sparse", runs="runs", key4="k4", nofilter="nf")[u] for u in units) + "}"
+        kernel = "k_match_{" + ",".join(dict(sparse="sparse", runs="runs", key4="k4", nofilter="nf",
+                                              uniform="uniform")[u] for u in units) + "}"
     key = f"{pmc_leg}:{kernel[2:]}" if kernel else None
     if pmc_leg and key in pmc:   # PMC passes ran on a whole 1 GiB shard; scale to this rank's launch
         traffic = pmc[key].get("hbm_bytes_per_launch") * n / pmc[key].get("input_bytes", GiB)

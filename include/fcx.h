@@ -152,15 +152,17 @@ int fcx_ctx_stats(fcx_ctx *ctx, uint64_t *tokens, uint64_t *matches, uint64_t *l
 /* The match kernel the last fcx_compress_shard call ran (routed: the unit given the most
  * tiles): 0 general, 1 4-byte keys (small alphabets), 2 without the repeat filter
  * (match-dense data), 3 run-mode walk inlined (long matches), 4 without the bucket search
- * (few matches); -1 for a NULL ctx. */
+ * (few matches), 5 the uniform unit (one byte value over the window); -1 for a NULL ctx. */
 int fcx_ctx_match_kernel(fcx_ctx *ctx);
 /* Routing of the last (routed) call, after a device synchronize: out[0..3] tiles filed to the
- * sparse, runs, 4-byte-key and no-filter units (the no-filter count includes the hand-ons), out[4]
- * tiles the sparse / runs units handed on to the no-filter unit, out[5] tiles with bytes, out[6]
- * tiles past the units' grids (searched by k_match_rest, the general kernel), out[7] 1 when the
- * call waited for its own counts (a context's first call).  Writes min(n, FCX_ROUTE_STATS)
- * values; FCX_ERR_ARG when the last call had a forced unit (fcx_ctx_set_match_mode). */
-#define FCX_ROUTE_STATS 8
+ * sparse, runs, 4-byte-key and no-filter units (the runs and no-filter counts include the tiles
+ * handed on to them), out[4] tiles handed on (sparse / runs units to the no-filter unit, the
+ * uniform unit to the runs unit), out[5] tiles with bytes, out[6] tiles past the units' grids
+ * (searched by the units' looped remainder kernels), out[7] 1 when the call waited for its own
+ * counts (a context's first call), out[8] tiles filed to the uniform unit (one byte value over
+ * the window: closed form).  Writes min(n, FCX_ROUTE_STATS) values; FCX_ERR_ARG when the last
+ * call had a forced unit (fcx_ctx_set_match_mode). */
+#define FCX_ROUTE_STATS 9
 int fcx_ctx_route_stats(fcx_ctx *ctx, uint64_t *out, int n);
 
 /* ---- GPU decoder ------------------------------------------------------------ */

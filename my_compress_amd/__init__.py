@@ -255,21 +255,23 @@ class Context:
         _check(lib().fcx_ctx_stats(self._h, *[ctypes.byref(v) for v in vals]), "fcx_ctx_stats")
         return dict(zip(["tokens", "matches", "lazy_evals", "lazy_tiles", "tiles"], [v.value for v in vals]))
 
-    MATCH_KERNELS = ("k_match", "k_match_k4", "k_match_nf", "k_match_runs", "k_match_sparse")
+    MATCH_KERNELS = ("k_match", "k_match_k4", "k_match_nf", "k_match_runs", "k_match_sparse", "k_match_uniform")
 
     def match_kernel(self) -> str:
         """the kernel the last compress_shard call's match stage ran (fcx_ctx_match_kernel; routed:
         the unit given the most tiles)"""
         return self.MATCH_KERNELS[lib().fcx_ctx_match_kernel(self._h)]
 
-    ROUTE_STATS = ("sparse", "runs", "key4", "nofilter", "handed_on", "tiles", "rest", "cold")
+    ROUTE_STATS = ("sparse", "runs", "key4", "nofilter", "handed_on", "tiles", "rest", "cold", "uniform")
 
     def route_stats(self) -> dict:
         """how the last (routed) call's tiles were searched (fcx_ctx_route_stats): tiles per unit
-        list, tiles the sparse / runs units handed on, tiles with bytes, tiles left to k_match_rest,
-        and whether the call waited for its own counts (a context's first call)"""
-        vals = (ctypes.c_uint64 * 8)()
-        _check(lib().fcx_ctx_route_stats(self._h, vals, 8), "fcx_ctx_route_stats")
+        list, tiles handed on (to the no-filter and runs lists), tiles with bytes, tiles left to the
+        units' remainder kernels, whether the call waited for its own counts (a context's first
+        call), and the uniform unit's tiles"""
+        n = len(self.ROUTE_STATS)
+        vals = (ctypes.c_uint64 * n)()
+        _check(lib().fcx_ctx_route_stats(self._h, vals, n), "fcx_ctx_route_stats")
         return dict(zip(self.ROUTE_STATS, [int(v) for v in vals]))
 
 

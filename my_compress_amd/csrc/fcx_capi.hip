@@ -38,6 +38,9 @@ FCX_REST_LAUNCHER(launch_match_rest_nf)
 void launch_classify(const uint8_t *in, const Layout &L, uint32_t *lists, uint32_t stride, uint32_t *cnt,
                      uint8_t *tkind, hipStream_t st);
 void launch_route_mark(uint32_t *dst, const uint32_t *src, hipStream_t st);
+void launch_match_uniform(const uint8_t *in, const Layout &L, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
+                          uint32_t *tinfo, const uint32_t *list, const uint32_t *cnt, uint32_t *runs_list,
+                          uint32_t *runs_cnt, uint32_t *hand_cnt, uint8_t *tkind, uint32_t grid, hipStream_t st);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -106,18 +109,17 @@ void set_last_error(const std::string &m) { g_err = m; }
 
 // the match kernel's translation units (fcx_match.hip and the fcx_match_<kind>.hip units that include it)
 enum MatchKernel : int {
-    kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2, kMatchRuns = 3, kMatchSparse = 4
+    kMatchAuto = -1, kMatchGeneral = 0, kMatchKey4 = 1, kMatchNoFilter = 2, kMatchRuns = 3, kMatchSparse = 4,
+    kMatchUniform = 5   // (fcx_ctx_match_kernel only: the uniform unit, fcx_match_uniform.hip, routed calls)
 };
 using MatchLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64_t *, uint64_t *, uint64_t *,
                              uint32_t *, uint32_t *, hipStream_t, uint32_t, const MatchRoute *, uint32_t);
 // routed calls (fcx_route.hip): the unit of each list, in launch order (the sparse and runs units hand
 // tiles on to the no-filter unit's list, so it comes last)
-constexpr int kRouteKernel[kRoutes] = {kMatchSparse, kMatchRuns, kMatchKey4, kMatchNoFilter};
-constexpr uint32_t kRouteWords = 8;         // device counters per block group (k_classify: cnt[0..5])
+constexpr int kRouteKernel[kSearchUnits] = {kMatchSparse, kMatchRuns, kMatchKey4, kMatchNoFilter};
 constexpr uint32_t kRouteMinTiles = 8;      // a unit expected to get fewer tiles is not launched (k_match_rest)
 constexpr uint32_t kRestGrid = 512;         // k_match_rest_<unit>'s workgroups (2 per CU: <= 128 VGPRs)
 constexpr uint32_t kRestDirect = ~0u;       // last_grid: a direct launch (its list's remainder starts at the cover)
-constexpr uint32_t kCoverWord = 6;          // route counter: the no-filter list's count at its listed launch
 constexpr uint64_t kRouteBytes = 4ull * kRouteWords * 8;   // route counters of kMaxGroups (= 8) groups
 constexpr uint64_t kWordBytes = 64 + kRouteBytes;          // dev_words
 static MatchLaunch match_launcher(int k) {
@@ -422,9 +424,9 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
         uint64_t cnt[kRoutes] = {}, valid = 0, fix = 0;
         for (uint32_t g = 0; g < kMaxGroups; g++) {
             for (uint32_t u = 0; u < kRoutes; u++) cnt[u] += __atomic_load_n(&hr[kRouteWords * g + u], __ATOMIC_RELAXED);
-            valid += __atomic_load_n(&hr[kRouteWords * g + 5], __ATOMIC_RELAXED);
+            valid += __atomic_load_n(&hr[kRouteWords * g + kRcValid], __ATOMIC_RELAXED);
             fix += __atomic_load_n(&hr[kRouteWords * g + kRouteNoFilter], __ATOMIC_RELAXED) -
-                   __atomic_load_n(&hr[kRouteWords * g + 4], __ATOMIC_RELAXED);
+                   __atomic_load_n(&hr[kRouteWords * g + kRcNfFiled], __ATOMIC_RELAXED);
         }
         fix += (uint32_t)__atomic_load_n(&c->host_words[2], __ATOMIC_RELAXED);   // lazy tiles (k_tree)
         if (valid) {
@@ -474,30 +476,38 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                 HIP_TRY(hipMemcpyAsync(cold, rc, 4 * kRouteWords, hipMemcpyDeviceToHost, sg));
                 HIP_TRY(hipStreamSynchronize(sg));
                 for (uint32_t u = 0; u < kRoutes; u++) { est[u] = cold[u]; cold_cnt[u] += cold[u]; }
-                cold_valid += cold[5];
+                cold_valid += cold[kRcValid];
             } else {
                 const uint64_t v = std::max<uint64_t>(c->hint_valid, 1);
                 for (uint32_t u = 0; u < kRoutes; u++) est[u] = (c->hint_cnt[u] * ntg + v - 1) / v;
             }
+            // the uniform unit first (looped: any grid covers its list; a multiple of 8 for its XCD split):
+            // the tiles it hands on join the runs list before any runs launch reads it.  At least 2048
+            // one-wave workgroups (≈ 3 µs when the list is empty), so an unforeseen list is still
+            // taken by 8 waves per CU
+            const uint32_t ugrid = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(2048, (est[kRouteUniform] + 7) / 8 * 8));
+            launch_match_uniform(gin, Lg, gmbits, gchain, gpfx, gtinfo, lists + (uint64_t)kRouteUniform * stride,
+                                 rc + kRouteUniform, lists + (uint64_t)kRouteRuns * stride, rc + kRouteRuns,
+                                 rc + kRcUniHandOn, c->tkind + t0, ugrid, sg);
             // the unit expected to take most of the tiles (at least half) runs first, direct over every
             // tile of the group: it drops the others by their kind byte -- or, when the estimate gives
             // it (nearly) all tiles, it searches every tile with the unrouted kernel's exact code, and
             // the few tiles of other kinds are searched again by their own units afterwards (the last
             // writer's outputs are complete).  The others run over their lists.
             uint32_t best = 0;
-            for (uint32_t u = 1; u < kRoutes; u++)
+            for (uint32_t u = 1; u < kSearchUnits; u++)
                 if (est[u] > est[best]) best = u;
             // (a recent call with hand-ons or lazy tiles -- tiles its units' samples misfiled -- keeps
             // every unit listed: only listed sparse / runs launches hand such tiles on)
             const bool direct = 2 * est[best] >= ntg && c->hint_fix == 0;
             const bool every = direct && 64 * est[best] >= 63ull * ntg;
-            uint32_t order[kRoutes], no = 0;
+            uint32_t order[kSearchUnits], no = 0;
             if (direct) order[no++] = best;
-            for (uint32_t u = 0; u < kRoutes; u++)
+            for (uint32_t u = 0; u < kSearchUnits; u++)
                 if (!(direct && u == best)) order[no++] = u;
-            MatchRoute rts[kRoutes];
-            RouteRest rest[kRoutes];
-            for (uint32_t q = 0; q < kRoutes; q++) {
+            MatchRoute rts[kSearchUnits];
+            RouteRest rest[kSearchUnits];
+            for (uint32_t q = 0; q < kSearchUnits; q++) {
                 const uint32_t u = order[q];
                 // a small margin over the estimate (its excess workgroups exit at once); the no-filter
                 // list also takes the tiles the sparse / runs units hand on
@@ -513,7 +523,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                     // the direct launch (first) has every entry of its list; the no-filter list grows by
                     // later hand-ons, past the entries the classifier filed (cnt[4])
                     rest[u].start = ~0u;
-                    if (u == kRouteNoFilter) rest[u].start_dev = rc + 4;
+                    if (u == kRouteNoFilter) rest[u].start_dev = rc + kRcNfFiled;
                     if (every) launch = MatchRoute{};   // (unrouted code: no kind check, no hand-on)
                 } else {
                     grid = (uint32_t)std::min<uint64_t>(gr, ntg);
@@ -523,8 +533,8 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                     if (u == kRouteNoFilter && grid) {
                         // covers min(grid, its count now); later hand-ons land past that count, possibly
                         // below the grid: its remainder starts at the smaller of the two
-                        launch_route_mark(rc + kCoverWord, rc + kRouteNoFilter, sg);
-                        rest[u].start_dev = rc + kCoverWord;
+                        launch_route_mark(rc + kRcCover, rc + kRouteNoFilter, sg);
+                        rest[u].start_dev = rc + kRcCover;
                     }
                 }
                 if (u == kRouteSparse || u == kRouteRuns) {
@@ -538,15 +548,16 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                 match_launcher(kRouteKernel[u])(gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, sg, 0u, &launch, grid);
                 c->last_grid[g][u] = direct && u == best ? kRestDirect : grid;
             }
-            if (g == 0) c->last_kernel = est[best] ? kRouteKernel[best] : kMatchGeneral;
+            if (g == 0)
+                c->last_kernel = est[kRouteUniform] > est[best] ? kMatchUniform : est[best] ? kRouteKernel[best] : kMatchGeneral;
             // each unit's remainder (the no-filter one last: it takes the others' hand-ons); a direct
             // sparse / runs / 4-byte launch leaves none
             using RestLaunch = void (*)(const uint8_t *, const Layout &, uint32_t *, uint64_t *, uint64_t *, uint64_t *,
                                         uint32_t *, uint32_t *, const RouteRest &, const MatchRoute &, uint32_t,
                                         hipStream_t);
-            const RestLaunch rest_launch[kRoutes] = {launch_match_rest_sparse, launch_match_rest_runs,
-                                                     launch_match_rest_k4, launch_match_rest_nf};
-            for (uint32_t u = 0; u < kRoutes; u++)
+            const RestLaunch rest_launch[kSearchUnits] = {launch_match_rest_sparse, launch_match_rest_runs,
+                                                          launch_match_rest_k4, launch_match_rest_nf};
+            for (uint32_t u = 0; u < kSearchUnits; u++)
                 if (rest[u].start != ~0u || rest[u].start_dev)
                     rest_launch[u](gin, Lg, gm, gmbits, gchain, gpfx, gtinfo, gmtok, rest[u], rts[u], kRestGrid, sg);
         }
@@ -644,17 +655,18 @@ int fcx_ctx_route_stats(fcx_ctx *c, uint64_t *out, int n) {
         HIP_TRY(hipMemcpy(rc, (uint8_t *)c->dev_words + 64, sizeof(rc), hipMemcpyDeviceToHost));
         for (uint32_t g = 0; g < c->last_groups; g++) {
             const uint32_t *r = rc + kRouteWords * g;
-            for (uint32_t u = 0; u < kRoutes; u++) {
+            for (uint32_t u = 0; u < kSearchUnits; u++) {
                 v[u] += r[u];
                 uint32_t s0 = c->last_grid[g][u] != kRestDirect ? c->last_grid[g][u]
-                              : u == kRouteNoFilter                ? r[4]
+                              : u == kRouteNoFilter                ? r[kRcNfFiled]
                                                                    : r[u];
                 if (u == kRouteNoFilter && c->last_grid[g][u] != kRestDirect && c->last_grid[g][u])
-                    s0 = std::min(s0, r[kCoverWord]);
+                    s0 = std::min(s0, r[kRcCover]);
                 v[6] += r[u] > s0 ? r[u] - s0 : 0u;
             }
-            v[4] += r[kRouteNoFilter] - r[4];
-            v[5] += r[5];
+            v[4] += r[kRouteNoFilter] - r[kRcNfFiled] + r[kRcUniHandOn];
+            v[5] += r[kRcValid];
+            v[8] += r[kRouteUniform];
         }
         v[7] = c->last_cold;
     }

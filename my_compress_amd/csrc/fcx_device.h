@@ -87,7 +87,19 @@ struct Layout {
 // ---- per-tile routing of the match search (fcx_route.hip) ------------------
 // k_classify sorts the shard's tiles into one list per match unit; each unit's kernel then runs over
 // its own list, so the unit that searches a tile depends only on that tile's bytes.
-enum : uint32_t { kRouteSparse = 0, kRouteRuns = 1, kRouteKey4 = 2, kRouteNoFilter = 3, kRoutes = 4 };
+// Lists 0-3 are the match units (fcx_match_<unit>.hip); list 4 the uniform unit (fcx_match_uniform.hip:
+// tiles whose sample is one byte value, checked over their whole window, the others handed on to runs).
+enum : uint32_t {
+    kRouteSparse = 0, kRouteRuns = 1, kRouteKey4 = 2, kRouteNoFilter = 3, kSearchUnits = 4,
+    kRouteUniform = 4, kRoutes = 5
+};
+// route counters per block group (k_classify, the units' hand-ons, the host's cover mark): [0, kRoutes)
+// list lengths, then these
+constexpr uint32_t kRcNfFiled = 5;    // tiles the classifier filed as no-filter (its list grows by hand-ons)
+constexpr uint32_t kRcValid = 6;      // tiles with bytes
+constexpr uint32_t kRcCover = 7;      // the no-filter list's length at its listed launch
+constexpr uint32_t kRcUniHandOn = 8;  // tiles the uniform unit handed on to the runs list
+constexpr uint32_t kRouteWords = 16;
 struct MatchRoute {
     const uint32_t *list = nullptr;   // the launch's tiles (null: the grid is every tile of the shard)
     const uint32_t *cnt = nullptr;    // entries in list

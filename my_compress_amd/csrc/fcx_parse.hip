@@ -473,14 +473,18 @@ __global__ __launch_bounds__(64) void k_stitch(const uint8_t *__restrict__ in, L
                     tile_off[3 * tixu + 1] = pm;
                     tile_off[3 * tixu + 2] = pg;
                     zero_edges_lane(s_flags, s_p, s_golomb, L, b, pt, pm, pg);
-                    uint64_t *cwu = chain + (uint64_t)b * L.wpb + (uint64_t)kk * (kTile / 64);
-                    const uint32_t nwu = (t1u - t0u + 63) / 64;
-                    for (uint32_t w = 0; w < nwu; w++) {
-                        const uint32_t lo = t0u + 64 * w;
-                        const uint32_t p = lo <= eu ? eu : eu + kStep * ((lo - eu + kStep - 1) / kStep);
-                        cwu[w] = p < min(lo + 64, t1u) ? 1ull << (p - lo) : 0ull;
-                    }
                     tconv[tixu] = kConvAll;
+                }
+                // the tiles' chain words, tile by tile with one word per lane (coalesced stores; one
+                // lane per tile looping over its 64 words stored 64 lines per instruction)
+                for (uint32_t i = 0; i < F; i++) {
+                    const uint32_t eui = (uint32_t)__builtin_amdgcn_readlane((int)eu, (int)i);
+                    const uint32_t t0i = (k + i) * kTile, t1i = min(blen, t0i + kTile), lo = t0i + 64 * lane;
+                    if (lo < t1i) {
+                        const uint32_t p = lo <= eui ? eui : eui + kStep * ((lo - eui + kStep - 1) / kStep);
+                        chain[(uint64_t)b * L.wpb + (uint64_t)(k + i) * (kTile / 64) + lane] =
+                            p < min(lo + 64, t1i) ? 1ull << (p - lo) : 0ull;
+                    }
                 }
                 const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)it, (int)(F - 1));
                 run.tok += tot;

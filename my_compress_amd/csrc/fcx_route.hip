@@ -6,6 +6,8 @@
 // choice is made per call from the call's input: k_classify reads a 128-byte sample at the start of
 // every 4096-position tile and files the tile into one list per unit, in tile order:
 //
+//   uniform   no byte change in the sample (zeros, padding): the uniform unit checks the whole
+//             window and writes the closed form, else hands the tile on to the runs list
 //   runs      few byte changes (≤ 1 per 8 sampled bytes: the tile's window then has ≲ 1024 runs
 //             and takes the run-mode closed form; zeros, runs)
 //   4-byte    ≤ 6 of the 64 byte-value buckets (v >> 2) seen ('ACGT' data: dense 3-byte keys)
@@ -34,8 +36,9 @@ constexpr uint32_t kClsWgTiles = kClsRound * kClsRounds;
 constexpr uint32_t kClsSample = 32 * kClsPerTile;        // 128 bytes sampled per tile (1/32 of the input)
 static_assert(kClsWgTiles <= kClsLanes, "one lane per tile for the ranks");
 
-// cnt: [0..3] list lengths (the no-filter list grows by the hand-ons later), [4] tiles the classifier
-// filed as no-filter, [5] tiles with bytes (a block's tail tiles past its length have none).
+// cnt: [0, kRoutes) list lengths (the no-filter and runs lists grow by the hand-ons later),
+// [kRcNfFiled] tiles the classifier filed as no-filter, [kRcValid] tiles with bytes (a block's tail
+// tiles past its length have none).
 // A workgroup takes kClsWgTiles consecutive tiles in rounds of kClsRound (the next round's sample
 // loads issued before this round's counting), then files them with one global atomic per list:
 // few workgroups (one per CU for a GiB), because atomics on one address from every XCD serialise in
@@ -121,7 +124,8 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
         const uint32_t buckets = (uint32_t)__builtin_popcount(slo) + (uint32_t)__builtin_popcount(shi);
         uint32_t kind = kRoutes;   // no bytes: no list
         if (len) {
-            if (8 * changes <= len) kind = kRouteRuns;
+            if (changes == 0 && len == kClsSample) kind = kRouteUniform;
+            else if (8 * changes <= len) kind = kRouteRuns;
             else if (buckets <= 6) kind = kRouteKey4;
             else if (buckets >= 40 && 16 * eq4 <= len) kind = kRouteSparse;
             else kind = kRouteNoFilter;
@@ -147,10 +151,10 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
         for (uint32_t q = 0; q < kClsWgTiles / 64; q++) tot += s_wsum[q][tid];
         if (tid < kRoutes) {
             s_base[tid] = tot ? atomicAdd(&cnt[tid], tot) : 0u;
-            if (tid == kRouteNoFilter && tot) atomicAdd(&cnt[4], tot);
+            if (tid == kRouteNoFilter && tot) atomicAdd(&cnt[kRcNfFiled], tot);
         } else {   // tiles with bytes: all but the no-list ones
             const uint32_t valid = kClsWgTiles - tot;   // (lanes past the shard's tiles count as no-list)
-            if (valid) atomicAdd(&cnt[5], valid);
+            if (valid) atomicAdd(&cnt[kRcValid], valid);
         }
     }
     __syncthreads();

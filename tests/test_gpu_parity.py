@@ -364,8 +364,9 @@ def test_key4_kernel_vs_oracle(cuda, block):
 
 @pytest.mark.parametrize("block", [1 << 20, 262144])
 def test_match_units_routed(cuda, block):
-    """text tiles go to the unit without the repeat filter, long-match tiles (runs, zeros) to the
-    runs unit, random data to the unit without the bucket search -- from a context's first call,
+    """text tiles go to the unit without the repeat filter, long-match tiles (runs) to the runs unit,
+    one-byte-value windows (zeros) to the uniform unit, random data to the unit without the bucket
+    search -- from a context's first call,
     decided by each tile's own bytes; the bytes equal the oracle's"""
     import torch
 
@@ -373,7 +374,7 @@ def test_match_units_routed(cuda, block):
     for name, data, want_kernel, lst in (("text", inputs.generate("text", 3, 3 << 20), 2, "nofilter"),
                                          ("rand", inputs.generate("rand", 4, 3 << 20), 4, "sparse"),
                                          ("runs", inputs.generate("runs", 5, 3 << 20), 3, "runs"),
-                                         ("zeros", bytes(3 << 20), 3, "runs"),
+                                         ("zeros", bytes(3 << 20), 5, "uniform"),
                                          ("mix", _small_alphabet_mix(9, 2 << 20), None, None)):
         want = oracle.compress_file(data, block)
         d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(cuda)
@@ -393,6 +394,9 @@ def test_match_units_routed(cuda, block):
                                           for b0 in range(0, len(data), block)), rs
                 if want_kernel is not None:
                     assert kernel(ctx._h) == want_kernel, (name, block, call)
-                    assert rs[lst] == rs["tiles"] and rs["rest"] == 0 and rs["handed_on"] == 0, (name, call, rs)
+                    # (a runs tile whose sample is one byte value goes to the uniform unit first, which
+                    # hands it on to the runs list: there every hand-on is one of those)
+                    assert rs[lst] == rs["tiles"] and rs["rest"] == 0, (name, call, rs)
+                    assert rs["handed_on"] == (rs["uniform"] if name == "runs" else 0), (name, call, rs)
         finally:
             ctx.close()

@@ -49,7 +49,7 @@ def test_mixed_blocks_every_unit(cuda, block):
             assert rs["tiles"] == len(data) // 4096
             # each kind is a quarter of the tiles (a few first-tiles of text blocks may file as sparse)
             assert abs(rs["sparse"] - q) <= 8 and rs["runs"] == q and rs["key4"] == q, rs
-            assert rs["sparse"] + rs["runs"] + rs["key4"] + rs["nofilter"] - rs["handed_on"] == rs["tiles"], rs
+            assert rs["sparse"] + rs["runs"] + rs["key4"] + rs["nofilter"] + rs["uniform"] - rs["handed_on"] == rs["tiles"], rs
             assert rs["cold"] == (call == 0), rs
             if call > 0:
                 assert rs["rest"] == 0, rs
@@ -199,3 +199,47 @@ def test_direct_every_tile_then_own_units(cuda):
             ctx.close()
             ref.close()
     assert _compress(mc.Context(0, block, len(txt)), cuda, txt, block) == oracle.compress_file(txt, block)
+
+
+def _uniform_cases():
+    """shards whose tiles the uniform unit takes, hands on, or shares with other units: whole zero /
+    0xAB blocks, zero runs that end inside a tile's window or look-ahead (sample uniform, window not:
+    handed on to the runs unit), a uniform stretch across a block boundary, text with zero holes, and
+    random data with page-sized zero stretches (the sparse unit direct over every tile as well)"""
+    rng = random.Random(17)
+    txt = inputs.generate("text", 90, 1 << 20)
+    rnd = inputs.generate("rand", 91, 4 << 20)
+    yield "zeros", bytes(3 << 20)
+    yield "ab", b"\xab" * ((2 << 20) + 5000)
+    parts = []   # every tile starts with 200..3000 zero bytes, then text
+    for t in range(512):
+        z = rng.randrange(200, 3000)
+        parts.append(bytes(z) + txt[t * 977 % (len(txt) - 4096):][: 4096 - z])
+    yield "zero_heads", b"".join(parts)
+    parts = []   # zero runs of 6..12 KiB ending at random offsets (inside later tiles' windows)
+    while sum(map(len, parts)) < (2 << 20):
+        parts.append(bytes(rng.randrange(6144, 12288)))
+        parts.append(txt[rng.randrange(0, len(txt) - 300):][: rng.randrange(1, 300)])
+    yield "zero_runs", b"".join(parts)
+    yield "holes", b"".join(txt[i:i + 65536] + bytes(rng.choice([4096, 8192, 9000, 20000])) for i in range(0, 1 << 20, 65536))
+    yield "rand_pages", b"".join(rnd[i:i + 500000] + bytes(rng.choice([8192, 16384, 12000])) for i in range(0, 4 << 20, 500000))
+
+
+@pytest.mark.parametrize("block", [1 << 20, 65536])
+def test_uniform_unit(cuda, block):
+    """the uniform unit (fcx_match_uniform.hip) against the oracle: closed-form tiles, hand-ons to the
+    runs unit where only the sample was uniform, and shards it shares with the other units"""
+    for name, data in _uniform_cases():
+        ctx = mc.Context(0, block, len(data))
+        try:
+            want = oracle.compress_file(data, block)
+            for call in range(2):
+                assert _compress(ctx, cuda, data, block) == want, (name, block, call)
+                rs = ctx.route_stats()
+                assert rs["sparse"] + rs["runs"] + rs["key4"] + rs["nofilter"] + rs["uniform"] - rs["handed_on"] == rs["tiles"], rs
+                if name in ("zeros", "ab"):
+                    assert rs["uniform"] == rs["tiles"] and rs["handed_on"] == 0, (name, rs)
+                if name == "zero_heads":   # every tile's sample is zeros, no window is: all handed on
+                    assert rs["uniform"] == rs["tiles"] and rs["handed_on"] >= rs["uniform"], (name, rs)
+        finally:
+            ctx.close()
