@@ -11,7 +11,7 @@ LEGS="${LEGS:-rand:rand:1048576:1024 c2:rand:65536:64 text:text:1048576:1024 c3:
 if [ -z "${SKIP_STATS:-}" ]; then
   for leg in $LEGS; do
     IFS=: read name kind block mib <<< "$leg"
-    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$name -o run --output-format csv -- python3 $R/bench.py --kind $kind --block $block --global-mib $mib --no-text --no-cpu-baseline --no-decode --no-host-path --no-lz78 > $R/gpurun_out/prof_$name.json 2> $R/gpurun_out/prof_$name.err) || exit 1
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$name -o run --output-format csv -- python3 $R/bench.py --kind $kind --block $block --global-mib $mib --no-text --no-cpu-baseline --no-decode --no-host-path --no-lz78 --no-transition > $R/gpurun_out/prof_$name.json 2> $R/gpurun_out/prof_$name.err) || exit 1
   done
 fi
 if [ -z "${SKIP_TRAFFIC:-}" ]; then
