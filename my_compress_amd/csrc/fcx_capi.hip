@@ -40,7 +40,7 @@ void launch_classify(const uint8_t *in, const Layout &L, uint32_t *lists, uint32
 void launch_route_mark(uint32_t *dst, const uint32_t *src, hipStream_t st);
 void launch_match_uniform(const uint8_t *in, const Layout &L, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                           uint32_t *tinfo, const uint32_t *list, const uint32_t *cnt, uint32_t *runs_list,
-                          uint32_t *runs_cnt, uint32_t *hand_cnt, uint8_t *tkind, uint32_t grid, hipStream_t st);
+                          uint32_t *runs_cnt, uint8_t *tkind, uint32_t grid, hipStream_t st);
 void launch_parse(const uint8_t *in, const Layout &L, uint32_t *m, const uint64_t *mbits, uint64_t *chain,
                   const uint64_t *chain_pfx, const uint32_t *tinfo, const uint32_t *mtok, uint64_t *fp,
                   uint32_t *tile_off, uint32_t *tconv, BlockInfo *binfo, uint8_t *s_flags, uint8_t *s_chars,
@@ -226,7 +226,7 @@ int ensure_scratch(fcx_ctx *c, uint64_t n) {
     if ((r = dalloc(&c->mbits, 8ull * nb * L.wpb, "mbits"))) return r;
     if ((r = dalloc(&c->chain_pfx, 8ull * (kTile / 64) * nt, "chain_pfx"))) return r;
     if ((r = dalloc(&c->tinfo, 32 * nt, "tinfo"))) return r;
-    if ((r = dalloc(&c->tile_off, 12 * nt, "tile_off"))) return r;
+    if ((r = dalloc(&c->tile_off, 12 * (nt + 1), "tile_off"))) return r;   // (+1: k_emit reads tile tix + 1's)
     if ((r = dalloc(&c->mtok, 4ull * kTileMatches * nt, "mtok"))) return r;
     if ((r = dalloc(&c->tconv, 4 * nt, "tconv"))) return r;
     if ((r = dalloc(&c->fp, 96 * nt, "fp"))) return r;   // 12 u64 per tile (k_resolve record)
@@ -488,7 +488,7 @@ int fcx_compress_shard(fcx_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_o
             const uint32_t ugrid = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(2048, (est[kRouteUniform] + 7) / 8 * 8));
             launch_match_uniform(gin, Lg, gmbits, gchain, gpfx, gtinfo, lists + (uint64_t)kRouteUniform * stride,
                                  rc + kRouteUniform, lists + (uint64_t)kRouteRuns * stride, rc + kRouteRuns,
-                                 rc + kRcUniHandOn, c->tkind + t0, ugrid, sg);
+                                 c->tkind + t0, ugrid, sg);
             // the unit expected to take most of the tiles (at least half) runs first, direct over every
             // tile of the group: it drops the others by their kind byte -- or, when the estimate gives
             // it (nearly) all tiles, it searches every tile with the unrouted kernel's exact code, and
@@ -664,7 +664,7 @@ int fcx_ctx_route_stats(fcx_ctx *c, uint64_t *out, int n) {
                     s0 = std::min(s0, r[kRcCover]);
                 v[6] += r[u] > s0 ? r[u] - s0 : 0u;
             }
-            v[4] += r[kRouteNoFilter] - r[kRcNfFiled] + r[kRcUniHandOn];
+            v[4] += r[kRouteNoFilter] - r[kRcNfFiled] + r[kRouteRuns] - r[kRcRunsFiled];
             v[5] += r[kRcValid];
             v[8] += r[kRouteUniform];
         }

@@ -98,7 +98,7 @@ enum : uint32_t {
 constexpr uint32_t kRcNfFiled = 5;    // tiles the classifier filed as no-filter (its list grows by hand-ons)
 constexpr uint32_t kRcValid = 6;      // tiles with bytes
 constexpr uint32_t kRcCover = 7;      // the no-filter list's length at its listed launch
-constexpr uint32_t kRcUniHandOn = 8;  // tiles the uniform unit handed on to the runs list
+constexpr uint32_t kRcRunsFiled = 8;  // tiles the classifier filed as runs (its list grows by the uniform unit's hand-ons)
 constexpr uint32_t kRouteWords = 16;
 struct MatchRoute {
     const uint32_t *list = nullptr;   // the launch's tiles (null: the grid is every tile of the shard)

@@ -138,10 +138,13 @@ __global__ __launch_bounds__(kTreeT) void k_tree(Layout L, const uint16_t *__res
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t b = blockIdx.x / kStreams, s = blockIdx.x % kStreams;
     BlockInfo &bi = binfo[b];
+    // (the record's fields this prologue tests, read together before its first branch)
+    const uint32_t lazy_tiles = bi.lazy_tiles, slen0 = bi.slen[0], gbits = bi.gbits;
+    asm volatile("" ::"s"(lazy_tiles), "s"(slen0), "s"(gbits));
     // the call's lazy tiles (k_stitch walked them serially), for the routing of later calls
     // (fcx_capi.hip: a unit that left tiles lazy is launched over its list, where hand-ons work)
-    if (s == 0 && tid == 0 && bi.lazy_tiles) atomicAdd(err + 2, bi.lazy_tiles);
-    if (!stream_active(bi, s)) {
+    if (s == 0 && tid == 0 && lazy_tiles) atomicAdd(err + 2, lazy_tiles);
+    if (s == 0 ? slen0 <= 1 : s == 3 ? gbits == 0 : false) {   // (stream_active)
         if (tid == 0) { bi.hdrlen[s] = 0; bi.nwords[s] = 0; }
         return;
     }

@@ -8,7 +8,8 @@
 // per tile checks the window from registers (seven 16-byte loads per lane) and writes the same
 // outputs: a tenth of the LDS-bound launch's cost on zeros.
 //
-// k_classify files a tile here when its 128-byte sample has no byte change; a tile whose window is not
+// k_classify files a tile here when its 128-byte sample has no byte change and the last dword of each
+// quarter of the tile holds the same byte; a tile whose window is not
 // uniform after all goes on to the runs list (the runs unit is launched after this kernel).  The kernel
 // is looped (few VGPRs: no occupancy cost), so any grid covers the whole list: each XCD takes a
 // contiguous eighth of it, so the overlapping windows of neighbouring tiles meet in that XCD's L2.
@@ -23,7 +24,7 @@ __global__ __launch_bounds__(64, 8) void k_match_uniform(const uint8_t *__restri
                                                       uint64_t *__restrict__ chain_pfx, uint32_t *__restrict__ tinfo,
                                                       const uint32_t *__restrict__ list, const uint32_t *__restrict__ cnt,
                                                       uint32_t *__restrict__ runs_list, uint32_t *__restrict__ runs_cnt,
-                                                      uint32_t *__restrict__ hand_cnt, uint8_t *__restrict__ tkind) {
+                                                      uint8_t *__restrict__ tkind) {
     const uint32_t lane = threadIdx.x;
     const uint32_t c = *cnt;
     const uint32_t xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;   // (grid: x 8)
@@ -47,9 +48,8 @@ __global__ __launch_bounds__(64, 8) void k_match_uniform(const uint8_t *__restri
         for (uint32_t r = 0; r < kUniLoads; r++) diff |= (w[r][0] ^ rep) | (w[r][1] ^ rep) | (w[r][2] ^ rep) | (w[r][3] ^ rep);
         if (__ballot(diff != 0)) {   // not one byte value: the runs unit searches it
             if (lane == 0) {
-                runs_list[atomicAdd(runs_cnt, 1u)] = bx;
-                atomicAdd(hand_cnt, 1u);
-                tkind[bx] = (uint8_t)kRouteRuns;
+                runs_list[atomicAdd(runs_cnt, 1u)] = bx;   // (one atomic: the count of these is the list's
+                tkind[bx] = (uint8_t)kRouteRuns;            //  growth past the classifier's kRcRunsFiled)
             }
             continue;
         }
@@ -106,9 +106,9 @@ __global__ __launch_bounds__(64, 8) void k_match_uniform(const uint8_t *__restri
 
 void launch_match_uniform(const uint8_t *in, const Layout &L, uint64_t *mbits, uint64_t *chain, uint64_t *chain_pfx,
                           uint32_t *tinfo, const uint32_t *list, const uint32_t *cnt, uint32_t *runs_list,
-                          uint32_t *runs_cnt, uint32_t *hand_cnt, uint8_t *tkind, uint32_t grid, hipStream_t st) {
+                          uint32_t *runs_cnt, uint8_t *tkind, uint32_t grid, hipStream_t st) {
     hipLaunchKernelGGL(k_match_uniform, dim3(grid), dim3(64), 0, st, in, L, mbits, chain, chain_pfx, tinfo, list, cnt,
-                       runs_list, runs_cnt, hand_cnt, tkind);
+                       runs_list, runs_cnt, tkind);
 }
 
 }  // namespace fcx

@@ -210,29 +210,28 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     if (t0 >= blen) return;
     const uint32_t t1 = min(blen, t0 + kTile);
     uint64_t *out = fp + (uint64_t)kFpStride * tix;
-    const uint32_t *ti = tinfo + 8ull * tix;
-    bool ok = (ti[0] & kTileLazy) == 0;
-    const bool uni = (ti[0] & kTileUniform) != 0;   // m = m_uniform, no rows
-    const uint32_t span = (ti[0] & kTileSpan2) ? kRmSpan : kResolveSpan;   // m rows exact below it
-    uint32_t ea = t0;
-    if (ok && k > 0) {
-        const uint32_t *tp = tinfo + 8ull * (tix - 1);
-        ok = (tp[0] & kTileLazy) == 0;
-        ea = tp[1];
-    }
-    ok = ok && ea < t1 && ea - t0 < span;
+    // this tile's flags, the previous one's flags and exit, and this tile's chain and mbits words (one
+    // per lane: in the block's words for every lane), all read before the first branch: the compiler
+    // does not move a load above one (the conditional form waited for six dependent round trips)
+    const uint32_t *ti = tinfo + 8ull * tix, *tp = tinfo + 8ull * (k > 0 ? tix - 1 : tix);
+    const uint32_t f0 = ti[0], pf0 = tp[0], pexit = tp[1];
+    const uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
+    const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
+    uint64_t wv = cw[lane], mv = mb[lane];
+    asm volatile("" ::"s"(f0), "s"(pf0), "s"(pexit), "v"(wv), "v"(mv));
+    const bool uni = (f0 & kTileUniform) != 0;   // m = m_uniform, no rows
+    const uint32_t span = (f0 & kTileSpan2) ? kRmSpan : kResolveSpan;   // m rows exact below it
+    const uint32_t ea = k > 0 ? pexit : t0;
+    bool ok = (f0 & kTileLazy) == 0 && (k == 0 || (pf0 & kTileLazy) == 0) && ea < t1 && ea - t0 < span;
     if (!ok) {
         if (lane == 0) out[0] = 0;
         return;
     }
     const uint32_t rel0 = ea - t0;
-    const uint64_t *cw = chain + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
-    const uint64_t *mb = mbits + (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64);
     const uint32_t *mt = m + bstart + t0;
     const uint32_t nw = min(span / 64, (t1 - t0 + 63) / 64);
-    // prefetch: chain + mbits words below the span (lanes 0..nw-1), m of those positions
-    uint64_t wv = 0, mv = 0;
-    if (lane < nw) { wv = cw[lane]; mv = mb[lane]; }
+    // chain + mbits words below the span (lanes 0..nw-1); m of those positions below
+    if (lane >= nw) { wv = 0; mv = 0; }
     // chain / mbits words stay distributed (lane q holds word q); the walk reads word q of the
     // wave-uniform position by readlane, and lane q keeps the walked bits of word q
     auto word_at = [](uint64_t v, uint32_t q) -> uint64_t {
@@ -795,29 +794,35 @@ __global__ __launch_bounds__(256) void k_emit(const uint8_t *__restrict__ in, La
     hc[tid] = 0;   // (every path's barriers order it)
     uint16_t *trow = thist + (uint64_t)tix * 256;
 
-    // ---- round 1: independent loads ----
+    // ---- round 1: independent loads.  Every scalar the tile needs is read unconditionally (tile_off
+    // has a tile of slack past the shard's last; every tile reads its block's record), and the check
+    // below combines its compares without short circuits: the compiler does not move a load above a
+    // branch, so the short-circuit form waited for seven dependent round trips before the first
+    // vector load.  The chain and mbits words are in the block's words for every lane. ----
     const bool last = t1 == blen;
-    const uint32_t tok0 = tile_off[3 * tix + 0], mi0 = tile_off[3 * tix + 1], g0 = tile_off[3 * tix + 2];
-    const uint32_t tk1 = last ? binfo[b].ntok : tile_off[3 * tix + 3];
-    const uint32_t mk1 = last ? binfo[b].nmatch : tile_off[3 * tix + 4];
     const uint32_t cv = tconv[tix];
-    const bool uni = (tinfo[8 * tix] & kTileUniform) != 0;   // m = m_uniform, no rows
-    const uint32_t nspec = tinfo[8 * tix + 3];   // match tokens of the speculative chain (its compact list)
+    const uint4 ti4 = *(const uint4 *)(tinfo + 8ull * tix);   // flags [0], match tokens of the speculative chain [3]
+    const uint32_t ti0 = ti4.x, nspec = ti4.w;
+    const uint32_t tok0 = tile_off[3 * tix + 0], mi0 = tile_off[3 * tix + 1], g0 = tile_off[3 * tix + 2];
+    const uint32_t tn0 = tile_off[3 * tix + 3], tn1 = tile_off[3 * tix + 4];
+    const uint32_t bnt = binfo[b].ntok, bnm = binfo[b].nmatch;
+    const uint32_t s = t0 + tid * 16;   // this lane's 16 positions: one quarter of a chain word
+    const uint64_t wi = (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2);
+    uint64_t cwv = chain[wi], mbv = mbits[wi];
+    asm volatile("" ::"s"(tok0), "s"(mi0), "s"(g0), "s"(tn0), "s"(tn1), "s"(bnt), "s"(bnm), "s"(cv), "s"(ti0), "s"(nspec),
+                 "v"(cwv), "v"(mbv));   // (all of them in flight before the check's branch)
+    const uint32_t tk1 = last ? bnt : tn0, mk1 = last ? bnm : tn1;
+    const bool uni = (ti0 & kTileUniform) != 0;   // m = m_uniform, no rows
     // the tile's offsets and counts come from scratch the earlier kernels wrote: one inconsistent
     // value (a kernel that did not run, a bug) sets an error bit instead of indexing the streams
     // or the match list out of bounds (uniform values: scalar compares)
-    if (tk1 > blen || tok0 > tk1 || tk1 - tok0 > t1 - t0 || mi0 > mk1 || mk1 - mi0 > tk1 - tok0 || mk1 > tk1 ||
-        nspec > kTileMatches || (cv >> 16) > kTileMatches || g0 > 8u * L.sstride[3]) {
+    const bool bad = (tk1 > blen) | (tok0 > tk1) | (tk1 - tok0 > t1 - t0) | (mi0 > mk1) | (mk1 - mi0 > tk1 - tok0) |
+                     (mk1 > tk1) | (nspec > kTileMatches) | ((cv >> 16) > kTileMatches) | (g0 > 8u * L.sstride[3]);
+    if (bad) {
         if (tid == 0) atomicOr(err, kErrScratch);
         return;
     }
-    const uint32_t s = t0 + tid * 16;   // this lane's 16 positions: one quarter of a chain word
-    uint64_t cwv = 0, mbv = 0;
-    if (s < t1) {
-        const uint64_t wi = (uint64_t)b * L.wpb + (uint64_t)k * (kTile / 64) + (tid >> 2);
-        cwv = chain[wi];
-        mbv = mbits[wi];
-    }
+    if (s >= t1) { cwv = 0; mbv = 0; }
     const uint8_t *d = in + bstart;
     const bool al = (((uintptr_t)d) & 15) == 0;
     // (the loads above are waited for by the check: a uniform tile -- zeros -- skips the input loads,

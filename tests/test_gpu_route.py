@@ -203,19 +203,24 @@ def test_direct_every_tile_then_own_units(cuda):
 
 def _uniform_cases():
     """shards whose tiles the uniform unit takes, hands on, or shares with other units: whole zero /
-    0xAB blocks, zero runs that end inside a tile's window or look-ahead (sample uniform, window not:
-    handed on to the runs unit), a uniform stretch across a block boundary, text with zero holes, and
-    random data with page-sized zero stretches (the sparse unit direct over every tile as well)"""
+    0xAB blocks, zero tiles with one other byte (samples uniform, window not: handed on to the runs
+    unit), zero runs that end inside a tile's window or look-ahead, a uniform stretch across a block boundary, text with zero holes, and
+    random data with page-sized zero stretches (the sparse unit direct over every tile as well)
+    (zero_specks: the sampled bytes are [0, 128) and the last dword of each 1 KiB quarter)"""
     rng = random.Random(17)
     txt = inputs.generate("text", 90, 1 << 20)
     rnd = inputs.generate("rand", 91, 4 << 20)
     yield "zeros", bytes(3 << 20)
     yield "ab", b"\xab" * ((2 << 20) + 5000)
-    parts = []   # every tile starts with 200..3000 zero bytes, then text
-    for t in range(512):
-        z = rng.randrange(200, 3000)
-        parts.append(bytes(z) + txt[t * 977 % (len(txt) - 4096):][: 4096 - z])
-    yield "zero_heads", b"".join(parts)
+    parts = []   # zero tiles with one 'A' each, away from the bytes k_classify samples: filed for the
+    for t in range(512):   # uniform unit, which finds the 'A' in the window and hands the tile on
+        tile = bytearray(4096)
+        x = rng.randrange(200, 4000)
+        while x % 1024 >= 1016:
+            x = rng.randrange(200, 4000)
+        tile[x] = 0x41
+        parts.append(bytes(tile))
+    yield "zero_specks", b"".join(parts)
     parts = []   # zero runs of 6..12 KiB ending at random offsets (inside later tiles' windows)
     while sum(map(len, parts)) < (2 << 20):
         parts.append(bytes(rng.randrange(6144, 12288)))
@@ -239,7 +244,7 @@ def test_uniform_unit(cuda, block):
                 assert rs["sparse"] + rs["runs"] + rs["key4"] + rs["nofilter"] + rs["uniform"] - rs["handed_on"] == rs["tiles"], rs
                 if name in ("zeros", "ab"):
                     assert rs["uniform"] == rs["tiles"] and rs["handed_on"] == 0, (name, rs)
-                if name == "zero_heads":   # every tile's sample is zeros, no window is: all handed on
+                if name == "zero_specks":   # every tile's samples are zeros, no window is: all handed on
                     assert rs["uniform"] == rs["tiles"] and rs["handed_on"] >= rs["uniform"], (name, rs)
         finally:
             ctx.close()
