@@ -8,8 +8,8 @@
 // per tile checks the window from registers (seven 16-byte loads per lane) and writes the same
 // outputs: a tenth of the LDS-bound launch's cost on zeros.
 //
-// k_classify files a tile here when its 128-byte sample has no byte change and the last dword of each
-// quarter of the tile holds the same byte; a tile whose window is not
+// k_classify files a tile here when its 128-byte sample has no byte change and the next tile of its
+// block starts with the same byte (that sample lies in this tile's look-ahead); a tile whose window is not
 // uniform after all goes on to the runs list (the runs unit is launched after this kernel).  The kernel
 // is looped (few VGPRs: no occupancy cost), so any grid covers the whole list: each XCD takes a
 // contiguous eighth of it, so the overlapping windows of neighbouring tiles meet in that XCD's L2.

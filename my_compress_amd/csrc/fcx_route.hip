@@ -47,6 +47,7 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
                                                         uint32_t *__restrict__ lists, uint32_t stride,
                                                         uint32_t *__restrict__ cnt, uint8_t *__restrict__ tkind) {
     __shared__ uint8_t s_kind[kClsWgTiles];
+    __shared__ uint16_t s_ub[kClsWgTiles];   // uniform sample: 0x100 | its byte, else 0
     __shared__ uint32_t s_wsum[kClsWgTiles / 64][kRoutes + 1];
     __shared__ uint32_t s_base[kRoutes];
     const uint32_t tid = threadIdx.x, tl = tid / kClsPerTile, sub = tid % kClsPerTile;
@@ -54,16 +55,11 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
     const uint32_t tile0 = blockIdx.x * kClsWgTiles;
     const uint32_t o = 32 * sub;   // this lane's sampled bytes [o, o + 32) of its tile
 
-    // sample of round r's tile (zero past len; len 0: no tile / no bytes), and one dword at the end of
-    // this lane's quarter of the tile (a sample without a byte change is filed for the uniform unit
-    // only when those four dwords hold its byte too: on runs data a 128-byte run is common, a
-    // tile-long one is not, and every misfiled tile costs the uniform unit a window read and a
-    // hand-on)
-    auto load = [&](uint32_t r, uint32_t (&w)[8], uint32_t &q4) -> uint32_t {
+    // sample of round r's tile (zero past len; len 0: no tile / no bytes)
+    auto load = [&](uint32_t r, uint32_t (&w)[8]) -> uint32_t {
         const uint32_t bx = tile0 + kClsRound * r + tl;
         uint32_t len = 0;
         const uint8_t *src = in;
-        q4 = 0;
         if (bx < nt) {
             const uint32_t b = bx / L.tpb, k = bx % L.tpb;
             const uint64_t bstart = (uint64_t)b * L.B;
@@ -71,12 +67,6 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
             if (t0 < blen) {
                 len = min(kClsSample, blen - t0);
                 src = in + bstart + t0;
-                const uint32_t tlen = min(kTile, blen - t0);
-                if (len == kClsSample) {   // (dword-aligned when the input is: one load)
-                    const uint8_t *q = src + ((min(kTile / kClsPerTile * (sub + 1), tlen) - 4) & ~3u);
-                    if ((((uintptr_t)q) & 3) == 0) q4 = *(const uint32_t *)q;
-                    else __builtin_memcpy(&q4, q, 4);
-                }
             }
         }
         if (o + 32 <= len && (((uintptr_t)(src + o)) & 15) == 0) {
@@ -95,9 +85,9 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
     };
     const uint32_t rounds = min(kClsRounds, (nt - tile0 + kClsRound - 1) / kClsRound);
     // every round's sample loads in flight at once (one memory latency per workgroup)
-    uint32_t ws[kClsRounds][8], lens[kClsRounds], q4s[kClsRounds];
+    uint32_t ws[kClsRounds][8], lens[kClsRounds];
 #pragma unroll
-    for (uint32_t r = 0; r < kClsRounds; r++) lens[r] = r < rounds ? load(r, ws[r], q4s[r]) : 0u;
+    for (uint32_t r = 0; r < kClsRounds; r++) lens[r] = r < rounds ? load(r, ws[r]) : 0u;
 #pragma unroll
     for (uint32_t r = 0; r < kClsRounds; r++) {
         if (r >= rounds) break;
@@ -124,9 +114,6 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
                 }
             }
         }
-        // the quarter-end dword against the tile's first byte (lane 0 of the tile's four holds it)
-        const uint32_t b0 = __shfl(w[0], lane & ~(kClsPerTile - 1), 64) & 0xFFu;
-        uint32_t qdiff = q4s[r] ^ (b0 * 0x01010101u);
         uint32_t slo = (uint32_t)seen, shi = (uint32_t)(seen >> 32);
 #pragma unroll
         for (uint32_t sft = 1; sft < kClsPerTile; sft <<= 1) {
@@ -134,22 +121,34 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
             eq4 += __shfl_xor(eq4, sft, 64);
             slo |= __shfl_xor(slo, sft, 64);
             shi |= __shfl_xor(shi, sft, 64);
-            qdiff |= __shfl_xor(qdiff, sft, 64);
         }
         const uint32_t buckets = (uint32_t)__builtin_popcount(slo) + (uint32_t)__builtin_popcount(shi);
         uint32_t kind = kRoutes;   // no bytes: no list
         if (len) {
-            if (changes == 0 && len == kClsSample && qdiff == 0) kind = kRouteUniform;
+            if (changes == 0 && len == kClsSample) kind = kRouteUniform;
             else if (8 * changes <= len) kind = kRouteRuns;
             else if (buckets <= 6) kind = kRouteKey4;
             else if (buckets >= 40 && 16 * eq4 <= len) kind = kRouteSparse;
             else kind = kRouteNoFilter;
         }
-        if (sub == 0) s_kind[kClsRound * r + tl] = (uint8_t)kind;
+        if (sub == 0) {
+            s_kind[kClsRound * r + tl] = (uint8_t)kind;
+            s_ub[kClsRound * r + tl] = kind == kRouteUniform ? (uint16_t)(0x100u | (w[0] & 0xFFu)) : (uint16_t)0;
+        }
     }
     __syncthreads();
-    // file the workgroup's tiles in tile order: lane t holds tile tile0 + t; ranks by ballot
-    const uint32_t kind = tid < rounds * kClsRound ? (uint32_t)s_kind[tid] : kRoutes;
+    // file the workgroup's tiles in tile order: lane t holds tile tile0 + t; ranks by ballot.  A uniform
+    // sample goes to the uniform unit only when the next tile of its block starts with the same byte
+    // too (that tile's sample lies inside this tile's look-ahead, so a uniform window has it; on runs
+    // data a 128-byte run is common, two at 4 KiB are not, and each misfiled tile costs the uniform
+    // unit a window read and a same-address atomic)
+    uint32_t kind = tid < rounds * kClsRound ? (uint32_t)s_kind[tid] : kRoutes;
+    if (kind == kRouteUniform && tid + 1 < kClsWgTiles && tile0 + tid + 1 < nt) {
+        const uint32_t bx = tile0 + tid, b = bx / L.tpb, k = bx % L.tpb;
+        const uint64_t bstart = (uint64_t)b * L.B;
+        const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
+        if (k + 1 < L.tpb && (k + 1) * kTile < blen && s_ub[tid + 1] != s_ub[tid]) kind = kRouteRuns;
+    }
     uint32_t rank = 0;
     if (tid < kClsWgTiles) {
 #pragma unroll

@@ -206,7 +206,7 @@ def _uniform_cases():
     0xAB blocks, zero tiles with one other byte (samples uniform, window not: handed on to the runs
     unit), zero runs that end inside a tile's window or look-ahead, a uniform stretch across a block boundary, text with zero holes, and
     random data with page-sized zero stretches (the sparse unit direct over every tile as well)
-    (zero_specks: the sampled bytes are [0, 128) and the last dword of each 1 KiB quarter)"""
+    (zero_specks: k_classify samples each tile's bytes [0, 128))"""
     rng = random.Random(17)
     txt = inputs.generate("text", 90, 1 << 20)
     rnd = inputs.generate("rand", 91, 4 << 20)
