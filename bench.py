@@ -754,8 +754,9 @@ def roofline(res, pmc_leg, pmc):
     # the match stage runs one of k_match's units (fcx_ctx_match_kernel): the kernel name is that unit's
     kernel = (res.get("match_kernel") or "k_match") if dom == "match" else f"k_{dom}" if dom else None
     rt = res.get("route") or {}
+    # (a unit counts when it searched at least 1 % of the tiles: a few misfiled samples handed on do not)
     units = [u for u in ("sparse", "runs", "key4", "nofilter", "uniform")
-             if rt.get(u, 0) - (rt.get("handed_on", 0) if u == "nofilter" else 0) > 0]
+             if 100 * (rt.get(u, 0) - (rt.get("handed_on", 0) if u == "nofilter" else 0)) >= rt.get("tiles", 0) > 0]
     if dom == "match" and len(units) > 1:   # routed over several units: the stage is their launches together
         kernel = "k_match_{" + ",".join(dict(sparse="sparse", runs="runs", key4="k4", nofilter="nf",
                                               uniform="uniform")[u] for u in units) + "}"

@@ -22,8 +22,19 @@ for leg, v in legs.items():
     avg = None
     if not os.path.exists(path):
         continue
-    for row in csv.DictReader(open(path)):
-        if row["Name"].split("(")[0].replace("void ", "").replace("fcx::", "").split("<")[0] == r["kernel"]:
+    rows = list(csv.DictReader(open(path)))
+    name = lambda row: row["Name"].split("(")[0].replace("void ", "").replace("fcx::", "").split("<")[0]
+    for row in rows:
+        if name(row) == r["kernel"]:
             avg = float(row["AverageNs"]) / 1e6
+    if avg is None and r["kernel"].startswith("k_match_{"):
+        # several units in one call: the match stage is the sum of the units' launches per call
+        # (their listed, direct and remainder kernels, the uniform unit), per k_classify call
+        calls = sum(int(row["Calls"]) for row in rows if name(row) == "k_classify")
+        tot = sum(float(row["TotalDurationNs"]) for row in rows if name(row).startswith("k_match") or name(row) == "k_route_mark")
+        avg = tot / max(calls, 1) / 1e6
+    if avg is None:
+        print(f"{leg:6s} {r['kernel']:10s} (no rocprof row)")
+        continue
     frac = r["alg_bytes_per_launch"] / (avg * 1e-3) / 1e9 / r["peak"]
     print(f"{leg:6s} {r['kernel']:10s} {r['kernel_ms']:15.3f} {avg:15.3f} {r['frac']:11.4f} {frac:13.4f}")
