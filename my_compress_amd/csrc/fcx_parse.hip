@@ -222,7 +222,9 @@ __global__ __launch_bounds__(64) void k_resolve(Layout L, const uint32_t *__rest
     const bool uni = (f0 & kTileUniform) != 0;   // m = m_uniform, no rows
     const uint32_t span = (f0 & kTileSpan2) ? kRmSpan : kResolveSpan;   // m rows exact below it
     const uint32_t ea = k > 0 ? pexit : t0;
-    bool ok = (f0 & kTileLazy) == 0 && (k == 0 || (pf0 & kTileLazy) == 0) && ea < t1 && ea - t0 < span;
+    // (a uniform tile's record is never used: k_stitch commits uniform tiles in closed form; skipping
+    // its walk took zeros' resolve + stitch from 0.207 to 0.117 ms per GiB)
+    bool ok = (f0 & (kTileLazy | kTileUniform)) == 0 && (k == 0 || (pf0 & kTileLazy) == 0) && ea < t1 && ea - t0 < span;
     if (!ok) {
         if (lane == 0) out[0] = 0;
         return;
