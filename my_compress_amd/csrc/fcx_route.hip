@@ -45,14 +45,16 @@ static_assert(kClsWgTiles <= kClsLanes, "one lane per tile for the ranks");
 // the fabric (256 lanes per 32 tiles and one atomic set per workgroup: 0.20-0.29 ms per GiB).
 __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restrict__ in, Layout L, uint32_t nt,
                                                         uint32_t *__restrict__ lists, uint32_t stride,
-                                                        uint32_t *__restrict__ cnt, uint8_t *__restrict__ tkind) {
+                                                        uint32_t *__restrict__ cnt, uint8_t *__restrict__ tkind,
+                                                        const uint32_t R) {
     __shared__ uint8_t s_kind[kClsWgTiles];
     __shared__ uint16_t s_ub[kClsWgTiles];   // uniform sample: 0x100 | its byte, else 0
     __shared__ uint32_t s_wsum[kClsWgTiles / 64][kRoutes + 1];
     __shared__ uint32_t s_base[kRoutes];
     const uint32_t tid = threadIdx.x, tl = tid / kClsPerTile, sub = tid % kClsPerTile;
     const uint32_t lane = tid & 63, wv = tid >> 6;
-    const uint32_t tile0 = blockIdx.x * kClsWgTiles;
+    const uint32_t wgt = kClsRound * R;   // this launch's tiles per workgroup (R <= kClsRounds rounds)
+    const uint32_t tile0 = blockIdx.x * wgt;
     const uint32_t o = 32 * sub;   // this lane's sampled bytes [o, o + 32) of its tile
 
     // sample of round r's tile (zero past len; len 0: no tile / no bytes)
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
         }
         return len;
     };
-    const uint32_t rounds = min(kClsRounds, (nt - tile0 + kClsRound - 1) / kClsRound);
+    const uint32_t rounds = min(R, (nt - tile0 + kClsRound - 1) / kClsRound);
     // every round's sample loads in flight at once (one memory latency per workgroup)
     uint32_t ws[kClsRounds][8], lens[kClsRounds];
 #pragma unroll
@@ -143,14 +145,14 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
     // data a 128-byte run is common, two at 4 KiB are not, and each misfiled tile costs the uniform
     // unit a window read and a same-address atomic)
     uint32_t kind = tid < rounds * kClsRound ? (uint32_t)s_kind[tid] : kRoutes;
-    if (kind == kRouteUniform && tid + 1 < kClsWgTiles && tile0 + tid + 1 < nt) {
+    if (kind == kRouteUniform && tid + 1 < rounds * kClsRound && tile0 + tid + 1 < nt) {
         const uint32_t bx = tile0 + tid, b = bx / L.tpb, k = bx % L.tpb;
         const uint64_t bstart = (uint64_t)b * L.B;
         const uint32_t blen = (uint32_t)min((uint64_t)L.B, L.n - bstart);
         if (k + 1 < L.tpb && (k + 1) * kTile < blen && s_ub[tid + 1] != s_ub[tid]) kind = kRouteRuns;
     }
     uint32_t rank = 0;
-    if (tid < kClsWgTiles) {
+    if (tid < wgt) {
 #pragma unroll
         for (uint32_t u = 0; u <= kRoutes; u++) {
             const uint64_t bal = __ballot(kind == u);
@@ -162,19 +164,19 @@ __global__ __launch_bounds__(kClsLanes) void k_classify(const uint8_t *__restric
     __syncthreads();
     if (tid <= kRoutes) {
         uint32_t tot = 0;
-        for (uint32_t q = 0; q < kClsWgTiles / 64; q++) tot += s_wsum[q][tid];
+        for (uint32_t q = 0; q < wgt / 64; q++) tot += s_wsum[q][tid];
         if (tid < kRoutes) {
             s_base[tid] = tot ? atomicAdd(&cnt[tid], tot) : 0u;
             if (tid == kRouteNoFilter && tot) atomicAdd(&cnt[kRcNfFiled], tot);
             if (tid == kRouteRuns && tot) atomicAdd(&cnt[kRcRunsFiled], tot);
         } else {   // tiles with bytes: all but the no-list ones
-            const uint32_t valid = kClsWgTiles - tot;   // (lanes past the shard's tiles count as no-list)
+            const uint32_t valid = wgt - tot;   // (lanes past the shard's tiles count as no-list)
             if (valid) atomicAdd(&cnt[kRcValid], valid);
         }
     }
     __syncthreads();
-    if (tid < kClsWgTiles && tile0 + tid < nt) tkind[tile0 + tid] = (uint8_t)kind;   // (the direct launch's filter)
-    if (tid < kClsWgTiles && kind < kRoutes) {
+    if (tid < wgt && tile0 + tid < nt) tkind[tile0 + tid] = (uint8_t)kind;   // (the direct launch's filter)
+    if (tid < wgt && kind < kRoutes) {
         uint32_t pos = s_base[kind] + rank;
         for (uint32_t q = 0; q < wv; q++) pos += s_wsum[q][kind];
         lists[(uint64_t)kind * stride + pos] = tile0 + tid;
@@ -195,8 +197,11 @@ void launch_route_mark(uint32_t *dst, const uint32_t *src, hipStream_t st) {
 void launch_classify(const uint8_t *in, const Layout &L, uint32_t *lists, uint32_t stride, uint32_t *cnt,
                      uint8_t *tkind, hipStream_t st) {
     const uint32_t nt = L.nblocks * L.tpb;
-    hipLaunchKernelGGL(k_classify, dim3((nt + kClsWgTiles - 1) / kClsWgTiles), dim3(kClsLanes), 0, st, in, L, nt,
-                       lists, stride, cnt, tkind);
+    // rounds per workgroup: 4 from 256 workgroups on (a GiB), fewer below, so a small shard (C2: 64 MiB)
+    // still spreads over 64 workgroups
+    const uint32_t R = std::min(kClsRounds, std::max(1u, nt / (256u * kClsRound)));
+    hipLaunchKernelGGL(k_classify, dim3((nt + kClsRound * R - 1) / (kClsRound * R)), dim3(kClsLanes), 0, st, in, L, nt,
+                       lists, stride, cnt, tkind, R);
 }
 
 }  // namespace fcx
