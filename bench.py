@@ -328,7 +328,7 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     total = state.get("total", seg_len)
     res = {
         "kind": kind, "block_bytes": block, "scaling": scaling, "global_bytes": n_global, "bytes_this_rank": n,
-        "out_bytes": total, "ratio": total / max(n_global, 1), "concat": concat,
+        "out_bytes": total, "ratio": total / max(n_global, 1), "concat": CONCAT_FORMS.get(concat, concat),
         "seconds": dt, "ms_per_step": dt / args.steps * 1e3, "value": n_global * args.steps / dt / 1e6,
         "compress_only": {"value": n_global * args.steps / dt_c / 1e6, "ms_per_step": dt_c / args.steps * 1e3,
                           "note": "device-resident compress of every rank's shard, no exchange (max over ranks)"},
@@ -738,6 +738,15 @@ def lz78_leg(dev, mib=1024, block=1 << 20, reps=2, ref_blocks=2):
             "cpu_baseline": {"value": ref_blocks * block / cpu_s / 1e6, "unit": "MB/s", "cores": 1,
                              "kind": "reference" if R is not None else "port",
                              "sample": f"first {ref_blocks} x {block // 1024} KiB blocks, my_compress_file_lz78"}}
+
+
+# the exchange each --concat form runs at N > 1 (named in the line's config)
+CONCAT_FORMS = {
+    "pipe": "pipe: each peer's segment sent to rank 0 in sub-batches as they finish (send/recv gather)",
+    "gather": "gather: every peer's whole segment sent to rank 0 after the compress (send/recv)",
+    "allgather": "allgather: every rank receives every segment (RCCL all-gather)",
+    "none": "none",
+}
 
 
 def roofline(res, pmc_leg, pmc):
