@@ -358,7 +358,7 @@ def run_leg(kind, seed, block, args, rank, world, dev, dist, profile_stages, sca
     if n:   # tiles per match unit in the last call (fcx_route.hip)
         res["route"] = ctx.route_stats()
     if n and kind in COLD_LEGS and (main_leg or world == 1):
-        res["cold_call"] = cold_call(d_in, n, d_out, cap, block, dev, res["compress_only"]["ms_per_step"])
+        res["cold_call"] = cold_call(d_in, n, cap, block, dev, res["compress_only"]["ms_per_step"])
     stats = ctx.stats() if n else {"tokens": 0, "matches": 0, "lazy_evals": 0, "lazy_tiles": 0}
     res["tokens"], res["matches"] = stats["tokens"], stats["matches"]
     res["lazy_evals"], res["lazy_tiles"] = stats["lazy_evals"], stats["lazy_tiles"]
@@ -430,7 +430,7 @@ def verify(kind, seed, block, n_global, scaling, rank, world, dev, dist, d_out, 
     return out
 
 
-def cold_call(d_in, n, d_out, cap, block, dev, steady_ms):
+def cold_call(d_in, n, cap, block, dev, steady_ms):
     """the first compress call of a fresh context (it waits for its own route counts: no estimate
     yet) and its second call, each synchronous, against the steady state of back-to-back calls"""
     import torch
@@ -439,6 +439,9 @@ def cold_call(d_in, n, d_out, cap, block, dev, steady_ms):
 
     ctx = mc.Context(dev.index, block, n)
     sid = torch.cuda.current_stream(dev).cuda_stream
+    # its own output buffer: d_out holds the step's assembled stream at N > 1 (rank 0's segment then
+    # the peers'), and a compress may write a few bytes past its segment's end (whole words)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     ms = []
     try:
         for _ in range(2):
