@@ -15,15 +15,17 @@
 //             buckets in 128 bytes, 1 in 256; text ~13 buckets)
 //   no-filter everything else (text, mixed)
 //
-// The counts are per-lane register work (no LDS atomics) reduced over the tile's 8 lanes by lane
+// The counts are per-lane register work (no LDS atomics) reduced over the tile's 4 lanes by lane
 // shuffles.
 //
 // A wrong guess costs time only.  The sparse and runs units hand a tile they cannot search in their
 // own modes to the no-filter unit's list (MatchRoute::defer_list), which is launched after them, so
-// no tile reaches the whole-tile run table it could overflow.  The host launches each unit over its
-// list with a grid estimated from the previous call (the counts come back asynchronously; a
-// context's first call waits for this call's counts instead), and k_match_rest, the general kernel
-// looped, takes the entries past each grid.  The output bytes do not depend on any of this.
+// no tile reaches the whole-tile run table it could overflow; the uniform unit hands a tile whose
+// window is not one byte value to the runs list.  The host launches each unit over its list with a
+// grid estimated from a recent call (the counts come back asynchronously; a context's first call
+// waits for this call's counts instead), and each unit's looped remainder kernel
+// (k_match_rest_<unit>) takes the entries past its grid.  The output bytes do not depend on any of
+// this.
 #include "fcx_device.h"
 
 namespace fcx {
